@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident LZF compress+decompress over batched
+value blocks (BASELINE.json "metric"), on N GPUs of one node.
+
+A *step* is one pass of the hot path over one batch of synthetic values
+already resident in HBM: lzf_gpu_compress_batch (out_len = n-4, the server
+policy of src/query.c:385) followed by lzf_gpu_decompress_batch of the
+results (out_len = n).  Values that do not compress are not decoded (as in
+the server, src/query.c:393-397).
+
+Default workload = BASELINE.json configs[1]: 1 M x 4 KiB JSON-like values per
+GPU.  Multi-GPU: one process per GPU (torchrun), values sharded round-robin
+(value i -> rank i mod N); no data-path collective, only a
+barrier and a max-over-ranks of the timings.  Weak scaling: every rank owns
+`count` values.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), including
+"roofline" for the dominant kernel (HIP events on the launch stream) and
+"cpu_baseline" (the reference codec compiled from /root/reference by
+oracle/Makefile, timed on this host's cores on a bounded sample; rank 0,
+N=1 only).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import gibson_amd  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+WORKLOADS = {
+    # name: (BASELINE config index, synth kind, seed, value bytes, values per GPU)
+    "json4k": (1, 1, 0x5EED0002, 4096, 1 << 20),
+    "text64k": (2, 2, 0x5EED0003, 65536, 1 << 18),
+    "text8k": (3, 0, 0x5EED0004, 8192, 1 << 20),
+    "mixed16k": (4, 3, 0x5EED0005, 16384, 1 << 20),
+}
+DESCR = {
+    "json4k": "1M x 4 KiB JSON-like values per GPU (BASELINE configs[1])",
+    "text64k": "256K x 64 KiB sentence-bank text per GPU (BASELINE configs[2])",
+    "text8k": "8 KiB Zipf text values (BASELINE configs[3] value shape)",
+    "mixed16k": "16 KiB mixed-entropy values (BASELINE configs[4] value shape)",
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="json4k", choices=sorted(WORKLOADS))
+    ap.add_argument("--count", type=int, default=0, help="values per GPU (default: workload's)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-count", type=int, default=0, help="CPU baseline sample values")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def cpu_baseline(kind, seed, n, count, threads):
+    """Time the CPU codec on a bounded sample (checker/baseline only)."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "cpu_bench_ref")
+    port = os.path.join(ROOT, "oracle", "cpu_bench")
+    exe = ref if os.path.exists(ref) else port
+    if not os.path.exists(exe):
+        return None
+    out = subprocess.run([exe, str(kind), str(n), str(count), str(threads), hex(seed), "5"],
+                         capture_output=True, text=True, timeout=600)
+    if out.returncode != 0:
+        return {"error": out.stderr.strip()[-200:]}
+    r = json.loads(out.stdout)
+    return {
+        "value": round(r["roundtrip_GBps"], 4),
+        "unit": "GB/s",
+        "cores": threads,
+        "kind": r["kind"],
+        "sample": f"{count} values x {n} B (first {count} of the workload's value indices), "
+                  f"compress+decompress, median of 5 after 1 warm-up, one value per OpenMP "
+                  f"thread; compress {r['compress_GBps']:.3f} GB/s, decompress "
+                  f"{r['decompress_GBps']:.3f} GB/s, ratio {r['comp_bytes'] / r['in_bytes']:.4f}",
+        "cpu": _cpu_model(),
+    }
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    cfg_idx, kind, seed, n, count = WORKLOADS[a.workload]
+    if a.count:
+        count = a.count
+
+    # ---- data in HBM: value i of this rank is global value rank + k*world ----
+    src = torch.empty(count * n, dtype=torch.uint8, device=dev)
+    gibson_amd.synth_fill(kind, seed, rank, world, count, n, src)
+    off = torch.arange(count, dtype=torch.int64, device=dev) * n
+    in_len = torch.full((count,), n, dtype=torch.int32, device=dev)
+    ccap = torch.full((count,), n - 4, dtype=torch.int32, device=dev)
+    comp = torch.empty(count * n, dtype=torch.uint8, device=dev)
+    clen = torch.zeros(count, dtype=torch.int32, device=dev)
+    dcap = torch.full((count,), n, dtype=torch.int32, device=dev)
+    dec = torch.empty(count * n, dtype=torch.uint8, device=dev)
+    dlen = torch.zeros(count, dtype=torch.int32, device=dev)
+    derr = torch.zeros(count, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+
+    ev = []
+
+    def step(record):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e2 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        gibson_amd.compress_batch(src, off, in_len, comp, off, ccap, clen, n, stream)
+        e1.record(stream)
+        # failed values (clen == 0) decode a 0-length stream: one control byte
+        # and an immediate error, i.e. they are skipped as in the server
+        gibson_amd.decompress_batch(comp, off, clen, dec, off, dcap, dlen, derr, n, stream)
+        e2.record(stream)
+        if record:
+            ev.append((e0, e1, e2))
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+
+    t_comp = sum(e0.elapsed_time(e1) for e0, e1, _ in ev) / a.steps / 1e3
+    t_dec = sum(e1.elapsed_time(e2) for _, e1, e2 in ev) / a.steps / 1e3
+    ok = clen > 0
+    n_ok = int(ok.sum())
+    c_bytes = int(clen.to(torch.int64).sum())
+    # sanity (outside the timed region): every compressed value decoded back
+    good = bool(torch.equal(dlen[ok], torch.full_like(dlen[ok], n)))
+    okm = ok.repeat_interleave(n)
+    good = good and bool(torch.equal(dec[okm], src[okm]))
+
+    stats = torch.tensor([wall, t_comp, t_dec], dtype=torch.float64, device=dev)
+    tot = torch.tensor([count * n, n_ok, c_bytes, 0 if good else 1], dtype=torch.float64,
+                       device=dev)
+    if world > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    wall, t_comp, t_dec = stats.tolist()
+    in_bytes_all, n_ok_all, c_bytes_all, bad_ranks = tot.tolist()
+
+    if rank == 0:
+        sec_per_step = wall / a.steps
+        value = in_bytes_all / sec_per_step / 1e9
+        # algorithmic bytes per launch, this rank
+        comp_bytes = count * n + c_bytes + 4 * count          # read N, write C + 4
+        dec_bytes = c_bytes + n_ok * n                          # read C, write N
+        kern = {
+            "lzf_compress": (comp_bytes, t_comp),
+            "lzf_decompress": (dec_bytes, t_dec),
+        }
+        dom = max(kern, key=lambda k: kern[k][1])
+        ach = kern[dom][0] / kern[dom][1] / 1e9
+        line = {
+            "metric": "LZF GB/s (device-resident) over batched value blocks, compress+decompress",
+            "value": round(value, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(sec_per_step * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": DESCR[a.workload],
+                "baseline_config": cfg_idx,
+                "values_per_gpu": count,
+                "value_bytes": n,
+                "out_len_policy": "n-4 (src/query.c:385)",
+                "sharding": "round-robin value i -> rank i mod N, no collective",
+                "compressed_fraction": round(n_ok_all / (count * world), 4),
+                "ratio": round(c_bytes_all / max(1.0, n_ok_all * n), 4),
+                "kernels": gibson_amd.kernel_info(),
+                "roundtrip_ok": bad_ranks == 0,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": dom,
+                "achieved": round(ach, 2),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBPS, 5),
+                "traffic": None,
+                "per_kernel_ms": {k: round(v[1] * 1e3, 3) for k, v in kern.items()},
+                "per_kernel_GBps": {k: round(v[0] / v[1] / 1e9, 2) for k, v in kern.items()},
+            },
+        }
+        if world == 1 and not a.no_cpu:
+            threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+            cnt = a.cpu_count or max(64, (256 << 20) // n)
+            line["cpu_baseline"] = cpu_baseline(kind, seed, n, cnt, threads)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

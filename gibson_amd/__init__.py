@@ -1,0 +1,23 @@
+"""gibson_amd -- MI355X-native LZF value codec for the Gibson cache server.
+
+The product is the C-ABI library ``gibson_amd/liblzf_hip.so`` (include/lzf.h
+drop-in + include/lzf_gpu.h batch API).  This package is the thin Python
+mirror of that boundary used by bench.py and the tests: ctypes bindings with
+the reference's names and semantics (``lzf_compress`` / ``lzf_decompress``,
+src/lzf.h:76-97) plus device-batch helpers over torch tensors (torch is only
+device-memory and stream plumbing here).
+"""
+from .lzf import (  # noqa: F401
+    LZF_VERSION,
+    LzfLibraryMissing,
+    compress_batch,
+    decompress_batch,
+    kernel_info,
+    lib,
+    lib_path,
+    lzf_compress,
+    lzf_decompress,
+    synth_fill,
+    host_compress_batch,
+    host_decompress_batch,
+)

@@ -1,0 +1,325 @@
+/*
+ * lzf_api.cpp -- the C-ABI of liblzf_hip.so.
+ *
+ * Exports the drop-in pair of include/lzf.h (replacing src/lzf_c.c:98 and
+ * src/lzf_d.c:55 behind the prototypes of src/lzf.h:76-78, 95-97) and the
+ * batched device API of include/lzf_gpu.h.  There is no CPU codec in this
+ * library: every call runs the HIP kernels; when no gfx950 device is
+ * usable the single-call entry points abort with a message (a GPU-backed
+ * codec without a GPU is a deployment error, not a silent fallback) and the
+ * batch calls return LZF_GPU_ENODEV.
+ *
+ * Single calls are batches of one.  Each calling thread owns a context
+ * (stream, device buffers, pinned staging), created lazily on the device
+ * named by LZF_GPU_DEVICE (default 0); the caller's current device is
+ * restored before returning, so Gibson's event loop never has to touch HIP.
+ */
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+
+#include "lzf_internal.h"
+#include "../../include/lzf.h"
+#include "../../include/lzf_gpu.h"
+
+hipError_t lzf_launch_compress_serial(const LzfBatch &b, hipStream_t s);
+hipError_t lzf_launch_decompress_serial(const LzfBatch &b, hipStream_t s);
+
+namespace {
+
+enum KernelGen { GEN_PARALLEL = 0, GEN_SERIAL = 1 };
+
+/* LZF_GPU_KERNEL=serial selects the single-lane generation (diagnostics,
+ * cross-checks); read per launch so one process can A/B both. */
+KernelGen kernel_gen()
+{
+    const char *e = getenv("LZF_GPU_KERNEL");
+    return (e && !strcmp(e, "serial")) ? GEN_SERIAL : GEN_PARALLEL;
+}
+
+bool device_ok(int dev)
+{
+    static std::mutex mu;
+    static int checked[64];      /* 0 unknown, 1 ok, -1 bad */
+    if (dev < 0 || dev >= 64) return false;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!checked[dev]) {
+        hipDeviceProp_t prop;
+        checked[dev] = (hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+                        strstr(prop.gcnArchName, "gfx950") != nullptr) ? 1 : -1;
+    }
+    return checked[dev] == 1;
+}
+
+int current_device_ok()
+{
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) return LZF_GPU_ENODEV;
+    return device_ok(dev) ? LZF_GPU_OK : LZF_GPU_ENODEV;
+}
+
+hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
+{
+    if (kernel_gen() == GEN_SERIAL || !lzf_compress_kernel_name())
+        return lzf_launch_compress_serial(b, s);
+    return lzf_launch_compress(b, s);
+}
+
+hipError_t launch_decompress(const LzfBatch &b, hipStream_t s)
+{
+    if (kernel_gen() == GEN_SERIAL || !lzf_decompress_kernel_name())
+        return lzf_launch_decompress_serial(b, s);
+    return lzf_launch_decompress(b, s);
+}
+
+[[noreturn]] void die(const char *what, hipError_t e)
+{
+    fprintf(stderr, "liblzf_hip: %s failed: %s -- no CPU fallback, aborting\n", what,
+            hipGetErrorString(e));
+    abort();
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) {
+            hipError_t e = hipSetDevice(dev);
+            if (e != hipSuccess) die("hipSetDevice", e);
+        }
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+/* Growable device / pinned buffers of one thread. */
+struct Buf {
+    void *p = nullptr;
+    size_t cap = 0;
+    bool pinned = false;
+    void *get(size_t need)
+    {
+        if (need == 0) need = 1;
+        if (need <= cap) return p;
+        size_t want = need + need / 4 + 256;
+        if (p) { pinned ? (void)hipHostFree(p) : (void)hipFree(p); }
+        p = nullptr;
+        cap = 0;
+        hipError_t e = pinned ? hipHostMalloc(&p, want, hipHostMallocDefault) : hipMalloc(&p, want);
+        if (e != hipSuccess) die(pinned ? "hipHostMalloc" : "hipMalloc", e);
+        cap = want;
+        return p;
+    }
+};
+
+struct Meta {               /* one value's descriptor, packed for one copy */
+    uint64_t in_off, out_off;
+    uint32_t in_len, out_cap, out_len;
+    int32_t err;
+};
+
+struct Ctx {
+    int dev = 0;
+    hipStream_t stream = nullptr;
+    Buf d_in, d_out, d_meta;
+    Buf h_in{nullptr, 0, true}, h_out{nullptr, 0, true}, h_meta{nullptr, 0, true};
+    Ctx()
+    {
+        const char *e = getenv("LZF_GPU_DEVICE");
+        dev = e ? atoi(e) : 0;
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || dev >= n || !device_ok(dev)) {
+            fprintf(stderr, "liblzf_hip: no gfx950 device %d (devices: %d) -- no CPU fallback, aborting\n",
+                    dev, n);
+            abort();
+        }
+        DeviceGuard g(dev);
+        hipError_t r = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+        if (r != hipSuccess) die("hipStreamCreate", r);
+    }
+};
+
+Ctx &ctx()
+{
+    static thread_local Ctx c;
+    return c;
+}
+
+void check(hipError_t e, const char *what)
+{
+    if (e != hipSuccess) die(what, e);
+}
+
+/* Host batch: stage arena + descriptors, run, copy back. */
+int host_batch(bool compress, const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+               uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len,
+               int32_t *err, uint32_t count)
+{
+    if (!count || !in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len)
+        return LZF_GPU_EARG;
+    Ctx &c = ctx();
+    DeviceGuard g(c.dev);
+    uint64_t in_end = 0, out_end = 0;
+    uint32_t max_len = 0;
+    for (uint32_t i = 0; i < count; i++) {
+        uint64_t ie = in_off[i] + (in_len[i] ? in_len[i] : 1u);   /* a 0-length stream reads 1 byte */
+        uint64_t oe = out_off[i] + out_cap[i];
+        if (ie > in_end) in_end = ie;
+        if (oe > out_end) out_end = oe;
+        uint32_t l = compress ? in_len[i] : out_cap[i];
+        if (l > max_len) max_len = l;
+    }
+    size_t meta_bytes = (size_t)count * (2 * sizeof(uint64_t) + 3 * sizeof(uint32_t) + sizeof(int32_t));
+    uint8_t *h_in = (uint8_t *)c.h_in.get(in_end);
+    uint8_t *h_meta = (uint8_t *)c.h_meta.get(meta_bytes);
+    uint8_t *d_in = (uint8_t *)c.d_in.get(in_end);
+    uint8_t *d_out = (uint8_t *)c.d_out.get(out_end);
+    uint8_t *d_meta = (uint8_t *)c.d_meta.get(meta_bytes);
+    memcpy(h_in, in, in_end);
+    uint64_t *m_in_off = (uint64_t *)h_meta;
+    uint64_t *m_out_off = m_in_off + count;
+    uint32_t *m_in_len = (uint32_t *)(m_out_off + count);
+    uint32_t *m_out_cap = m_in_len + count;
+    uint32_t *m_out_len = m_out_cap + count;
+    int32_t *m_err = (int32_t *)(m_out_len + count);
+    memcpy(m_in_off, in_off, count * sizeof(uint64_t));
+    memcpy(m_out_off, out_off, count * sizeof(uint64_t));
+    memcpy(m_in_len, in_len, count * sizeof(uint32_t));
+    memcpy(m_out_cap, out_cap, count * sizeof(uint32_t));
+    size_t res_off = (uint8_t *)m_out_len - h_meta;
+    check(hipMemcpyAsync(d_in, h_in, in_end, hipMemcpyHostToDevice, c.stream), "hipMemcpyAsync");
+    check(hipMemcpyAsync(d_meta, h_meta, res_off, hipMemcpyHostToDevice, c.stream), "hipMemcpyAsync");
+    LzfBatch b;
+    b.in = d_in;
+    b.in_off = (const uint64_t *)d_meta;
+    b.out_off = b.in_off + count;
+    b.in_len = (const uint32_t *)(b.out_off + count);
+    b.out_cap = b.in_len + count;
+    b.out_len = (uint32_t *)(b.out_cap + count);
+    b.err = (int32_t *)(b.out_len + count);
+    b.out = d_out;
+    b.count = count;
+    b.max_len = max_len;
+    check(compress ? launch_compress(b, c.stream) : launch_decompress(b, c.stream), "kernel launch");
+    check(hipMemcpyAsync(h_meta + res_off, d_meta + res_off, meta_bytes - res_off,
+                         hipMemcpyDeviceToHost, c.stream), "hipMemcpyAsync");
+    check(hipStreamSynchronize(c.stream), "hipStreamSynchronize");
+    memcpy(out_len, m_out_len, count * sizeof(uint32_t));
+    if (err) memcpy(err, m_err, count * sizeof(int32_t));
+    /* copy back only the produced bytes of each value */
+    uint64_t lo = ~0ull, hi = 0;
+    for (uint32_t i = 0; i < count; i++) {
+        if (!m_out_len[i]) continue;
+        if (out_off[i] < lo) lo = out_off[i];
+        if (out_off[i] + m_out_len[i] > hi) hi = out_off[i] + m_out_len[i];
+    }
+    if (hi > lo) {
+        uint8_t *h_out = (uint8_t *)c.h_out.get(hi - lo);
+        check(hipMemcpyAsync(h_out, d_out + lo, hi - lo, hipMemcpyDeviceToHost, c.stream),
+              "hipMemcpyAsync");
+        check(hipStreamSynchronize(c.stream), "hipStreamSynchronize");
+        for (uint32_t i = 0; i < count; i++)
+            if (m_out_len[i]) memcpy(out + out_off[i], h_out + (out_off[i] - lo), m_out_len[i]);
+    }
+    return LZF_GPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+unsigned int lzf_compress(const void *const in_data, unsigned int in_len, void *out_data,
+                          unsigned int out_len)
+{
+    if (!in_len || !out_len) return 0;                    /* src/lzf_c.c:131 */
+    uint64_t zero = 0;
+    uint32_t res = 0;
+    host_batch(true, (const uint8_t *)in_data, &zero, &in_len, (uint8_t *)out_data, &zero,
+               &out_len, &res, nullptr, 1);
+    return res;
+}
+
+unsigned int lzf_decompress(const void *const in_data, unsigned int in_len, void *out_data,
+                            unsigned int out_len)
+{
+    uint64_t zero = 0;
+    uint32_t res = 0;
+    int32_t err = 0;
+    host_batch(false, (const uint8_t *)in_data, &zero, &in_len, (uint8_t *)out_data, &zero,
+               &out_len, &res, &err, 1);
+    if (!res) errno = err;
+    return res;
+}
+
+int lzf_gpu_compress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                           uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                           uint32_t *out_len, uint32_t count, uint32_t max_in_len, void *stream)
+{
+    if (!count || !in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len)
+        return LZF_GPU_EARG;
+    if (max_in_len > LZF_GPU_MAX_VALUE) return LZF_GPU_EARG;
+    int rc = current_device_ok();
+    if (rc) return rc;
+    LzfBatch b{in, in_off, in_len, out, out_off, out_cap, out_len, nullptr, count, max_in_len};
+    return launch_compress(b, (hipStream_t)stream) == hipSuccess ? LZF_GPU_OK : LZF_GPU_ELAUNCH;
+}
+
+int lzf_gpu_decompress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                             uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                             uint32_t *out_len, int32_t *err, uint32_t count,
+                             uint32_t max_out_cap, void *stream)
+{
+    if (!count || !in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len || !err)
+        return LZF_GPU_EARG;
+    int rc = current_device_ok();
+    if (rc) return rc;
+    LzfBatch b{in, in_off, in_len, out, out_off, out_cap, out_len, err, count, max_out_cap};
+    return launch_decompress(b, (hipStream_t)stream) == hipSuccess ? LZF_GPU_OK : LZF_GPU_ELAUNCH;
+}
+
+int lzf_gpu_synth_fill(int kind, uint64_t seed, uint64_t first, uint64_t stride, uint32_t count,
+                       uint32_t n, uint8_t *out, void *stream)
+{
+    if (!count || !n || !out || kind < 0) return LZF_GPU_EARG;
+    int rc = current_device_ok();
+    if (rc) return rc;
+    return lzf_launch_synth(kind, seed, first, stride, count, n, out, (hipStream_t)stream) ==
+                   hipSuccess
+               ? LZF_GPU_OK
+               : LZF_GPU_ELAUNCH;
+}
+
+int lzf_host_compress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                            uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                            uint32_t *out_len, uint32_t count)
+{
+    return host_batch(true, in, in_off, in_len, out, out_off, out_cap, out_len, nullptr, count);
+}
+
+int lzf_host_decompress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                              uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                              uint32_t *out_len, int32_t *err, uint32_t count)
+{
+    return host_batch(false, in, in_off, in_len, out, out_off, out_cap, out_len, err, count);
+}
+
+const char *lzf_gpu_kernel_info(void)
+{
+    static thread_local std::string s;
+    bool ser = kernel_gen() == GEN_SERIAL;
+    const char *c = lzf_compress_kernel_name();
+    const char *d = lzf_decompress_kernel_name();
+    s = std::string("compress=") + ((ser || !c) ? "serial" : c) +
+        " decompress=" + ((ser || !d) ? "serial" : d);
+    return s.c_str();
+}
+
+}  // extern "C"

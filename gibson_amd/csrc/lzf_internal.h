@@ -1,0 +1,40 @@
+/*
+ * lzf_internal.h -- shared definitions between the HIP kernels and the
+ * C-ABI layer (lzf_api.cpp).  Not installed; the public boundary is
+ * include/lzf.h and include/lzf_gpu.h.
+ */
+#ifndef GIBSON_AMD_LZF_INTERNAL_H
+#define GIBSON_AMD_LZF_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+/* LZF format constants (reference src/lzf_c.c:74-76, src/lzfP.h:55) */
+#define LZF_MAX_LIT   32u
+#define LZF_WINDOW    8192u
+#define LZF_MAX_REF   264u
+#define LZF_SLOTS     65536u
+
+/* one batch, device pointers */
+struct LzfBatch {
+    const uint8_t *in;
+    const uint64_t *in_off;
+    const uint32_t *in_len;
+    uint8_t *out;
+    const uint64_t *out_off;
+    const uint32_t *out_cap;
+    uint32_t *out_len;
+    int32_t *err;          /* decompress only */
+    uint32_t count;
+    uint32_t max_len;      /* max in_len (compress) / max out_cap (decompress) */
+};
+
+/* launchers, defined next to their kernels; return hipSuccess or the error */
+hipError_t lzf_launch_compress(const LzfBatch &b, hipStream_t s);
+hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s);
+hipError_t lzf_launch_synth(int kind, uint64_t seed, uint64_t first, uint64_t stride,
+                            uint32_t count, uint32_t n, uint8_t *out, hipStream_t s);
+const char *lzf_compress_kernel_name(void);
+const char *lzf_decompress_kernel_name(void);
+
+#endif

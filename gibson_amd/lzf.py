@@ -1,0 +1,163 @@
+"""ctypes mirror of liblzf_hip.so (include/lzf.h, include/lzf_gpu.h).
+
+Names, argument meaning and error behaviour follow the reference API:
+``lzf_compress(in, out_len)`` returns the stream or ``None`` (the C call's 0,
+src/lzf_c.c:131/176/263/276); ``lzf_decompress(in, out_len)`` returns
+``(bytes, 0)`` or ``(None, errno)`` with errno E2BIG / EINVAL in the order of
+src/lzf_d.c:72-131.  There is no Python or CPU codec behind these names: a
+missing or unloadable library raises ``LzfLibraryMissing``.
+"""
+import ctypes
+import os
+
+LZF_VERSION = 0x0105  # src/lzf.h:49
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+LZF_GPU_OK = 0
+_ERRS = {-1: "EARG", -2: "ELAUNCH", -3: "ENODEV", -4: "ENOMEM"}
+
+EXPORTS = (
+    "lzf_compress",
+    "lzf_decompress",
+    "lzf_gpu_compress_batch",
+    "lzf_gpu_decompress_batch",
+    "lzf_gpu_synth_fill",
+    "lzf_host_compress_batch",
+    "lzf_host_decompress_batch",
+    "lzf_gpu_kernel_info",
+)
+
+
+class LzfLibraryMissing(ImportError):
+    pass
+
+
+def lib_path():
+    return os.path.join(_HERE, "liblzf_hip.so")
+
+
+def lib():
+    """Load liblzf_hip.so (built in-tree by __graft_entry__.build())."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = lib_path()
+    if not os.path.exists(path):
+        raise LzfLibraryMissing(f"{path} not built: run __graft_entry__.build() "
+                                "(make -C gibson_amd/csrc); there is no CPU fallback")
+    try:
+        L = ctypes.CDLL(path, use_errno=True)
+    except OSError as e:
+        raise LzfLibraryMissing(f"cannot load {path}: {e}") from e
+    u32, u64, vp, i32 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int32
+    L.lzf_compress.restype = ctypes.c_uint
+    L.lzf_compress.argtypes = [vp, ctypes.c_uint, vp, ctypes.c_uint]
+    L.lzf_decompress.restype = ctypes.c_uint
+    L.lzf_decompress.argtypes = [vp, ctypes.c_uint, vp, ctypes.c_uint]
+    L.lzf_gpu_compress_batch.restype = ctypes.c_int
+    L.lzf_gpu_compress_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, u32, vp]
+    L.lzf_gpu_decompress_batch.restype = ctypes.c_int
+    L.lzf_gpu_decompress_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, u32, vp]
+    L.lzf_gpu_synth_fill.restype = ctypes.c_int
+    L.lzf_gpu_synth_fill.argtypes = [ctypes.c_int, u64, u64, u64, u32, u32, vp, vp]
+    L.lzf_host_compress_batch.restype = ctypes.c_int
+    L.lzf_host_compress_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32]
+    L.lzf_host_decompress_batch.restype = ctypes.c_int
+    L.lzf_host_decompress_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32]
+    L.lzf_gpu_kernel_info.restype = ctypes.c_char_p
+    L.lzf_gpu_kernel_info.argtypes = []
+    del i32
+    _LIB = L
+    return L
+
+
+def kernel_info():
+    return lib().lzf_gpu_kernel_info().decode()
+
+
+def _check(rc, what):
+    if rc != LZF_GPU_OK:
+        raise RuntimeError(f"{what} failed: {_ERRS.get(rc, rc)}")
+
+
+# ---- single-call drop-in (src/lzf.h:76-97) -------------------------------
+
+def lzf_compress(data, out_len):
+    """Compress ``data`` into at most ``out_len`` bytes; None if it does not fit."""
+    data = bytes(data)
+    src = ctypes.create_string_buffer(data, max(len(data), 1))
+    dst = ctypes.create_string_buffer(max(out_len, 1))
+    r = lib().lzf_compress(src, len(data), dst, out_len)
+    return dst.raw[:r] if r else None
+
+
+def lzf_decompress(data, out_len):
+    """Decode ``data``; returns (bytes, 0) or (None, errno)."""
+    data = bytes(data)
+    # the reference reads one control byte even when in_len == 0
+    src = ctypes.create_string_buffer(data + b"\xff", len(data) + 1)
+    dst = ctypes.create_string_buffer(max(out_len, 1))
+    ctypes.set_errno(0)
+    r = lib().lzf_decompress(src, len(data), dst, out_len)
+    if r:
+        return dst.raw[:r], 0
+    return None, ctypes.get_errno()
+
+
+# ---- device batches over torch tensors -------------------------------------
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream_handle(stream):
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def compress_batch(inp, in_off, in_len, out, out_off, out_cap, out_len, max_in_len, stream=None):
+    """Device batch compress; all tensors on the same CUDA (HIP) device.
+    inp/out uint8, *_off int64, in_len/out_cap/out_len int32 (read as u32)."""
+    n = in_len.numel()
+    rc = lib().lzf_gpu_compress_batch(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out),
+                                      _ptr(out_off), _ptr(out_cap), _ptr(out_len), n,
+                                      int(max_in_len), _stream_handle(stream))
+    _check(rc, "lzf_gpu_compress_batch")
+
+
+def decompress_batch(inp, in_off, in_len, out, out_off, out_cap, out_len, err, max_out_cap,
+                     stream=None):
+    n = in_len.numel()
+    rc = lib().lzf_gpu_decompress_batch(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out),
+                                        _ptr(out_off), _ptr(out_cap), _ptr(out_len), _ptr(err),
+                                        n, int(max_out_cap), _stream_handle(stream))
+    _check(rc, "lzf_gpu_decompress_batch")
+
+
+def synth_fill(kind, seed, first, stride, count, n, out, stream=None):
+    rc = lib().lzf_gpu_synth_fill(int(kind), int(seed), int(first), int(stride), int(count),
+                                  int(n), _ptr(out), _stream_handle(stream))
+    _check(rc, "lzf_gpu_synth_fill")
+
+
+def _np_ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def host_compress_batch(inp, in_off, in_len, out, out_off, out_cap, out_len):
+    """Host-memory batch (numpy arrays): PCIe staging inside the library."""
+    rc = lib().lzf_host_compress_batch(_np_ptr(inp), _np_ptr(in_off), _np_ptr(in_len),
+                                       _np_ptr(out), _np_ptr(out_off), _np_ptr(out_cap),
+                                       _np_ptr(out_len), len(in_len))
+    _check(rc, "lzf_host_compress_batch")
+
+
+def host_decompress_batch(inp, in_off, in_len, out, out_off, out_cap, out_len, err):
+    rc = lib().lzf_host_decompress_batch(_np_ptr(inp), _np_ptr(in_off), _np_ptr(in_len),
+                                         _np_ptr(out), _np_ptr(out_off), _np_ptr(out_cap),
+                                         _np_ptr(out_len), _np_ptr(err), len(in_len))
+    _check(rc, "lzf_host_decompress_batch")

@@ -1,0 +1,96 @@
+/*
+ * lzf_gpu.h -- batched, device-resident LZF API of liblzf_hip.so.
+ *
+ * The reference has no batch entry point: it calls lzf_compress once per
+ * SET/MSET key (src/query.c:391, reached from src/query.c:453 and :500) and
+ * lzf_decompress once per GET/MGET item (src/net.c:1229, src/net.c:1309).
+ * These calls take a whole batch of independent values at once; each value
+ * gets exactly the single-call semantics of src/lzf_c.c / src/lzf_d.c
+ * (results bit-identical to the reference, per-value return value and
+ * errno), so the single-call drop-in in lzf.h is a batch of one.
+ *
+ * Layout: values are addressed by (offset, length) pairs into one byte
+ * arena per direction.  Every pointer passed to lzf_gpu_* is DEVICE memory
+ * (hipMalloc'd, or torch CUDA tensors); `stream` is a hipStream_t (NULL =
+ * the legacy default stream).  Calls are asynchronous on `stream`.
+ *
+ * Return value of every call: LZF_GPU_OK or a negative LZF_GPU_E* code
+ * (the launch was not made).
+ */
+#ifndef LZF_GPU_H
+#define LZF_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LZF_GPU_OK          0
+#define LZF_GPU_EARG       -1   /* bad argument (NULL pointer, count 0 ...) */
+#define LZF_GPU_ELAUNCH    -2   /* HIP launch / copy failed */
+#define LZF_GPU_ENODEV     -3   /* no usable gfx950 device */
+#define LZF_GPU_ENOMEM     -4   /* device / pinned allocation failed */
+
+/* Largest value the batch kernels take in one piece (bytes).  Gibson's
+ * default max_value_size is far below it (src/default.h:52) and the shipped
+ * config's 2 MiB (debian/etc/gibson/gibson.conf:33) too. */
+#define LZF_GPU_MAX_VALUE  (64u << 20)
+
+/*
+ * Compress `count` values.  Value i is in[in_off[i] .. +in_len[i]); its
+ * stream is written to out[out_off[i] .. +out_cap[i]) and its length to
+ * out_len[i] (0 = does not fit, exactly when src/lzf_c.c returns 0; the
+ * bytes at out then are unspecified, and nothing is ever written at or past
+ * out_cap[i]).  max_in_len is an upper bound on every in_len[i] (selects the
+ * kernel's LDS plan without reading device memory).
+ * The server policy of src/query.c:385 is out_cap[i] = in_len[i] - 4.
+ */
+int lzf_gpu_compress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                           uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                           uint32_t *out_len, uint32_t count, uint32_t max_in_len,
+                           void *stream);
+
+/*
+ * Decompress `count` streams.  Stream i is in[in_off[i] .. +in_len[i]);
+ * the decoded bytes go to out[out_off[i] .. +out_cap[i]); out_len[i] gets
+ * the decoded length or 0, err[i] gets 0, E2BIG or EINVAL exactly as the
+ * reference sets errno (src/lzf_d.c:72-131).  As in the reference, a stream
+ * with in_len 0 still reads its first control byte, so in[in_off[i]] must be
+ * readable.  max_out_cap bounds every out_cap[i].
+ */
+int lzf_gpu_decompress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                             uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                             uint32_t *out_len, int32_t *err, uint32_t count,
+                             uint32_t max_out_cap, void *stream);
+
+/*
+ * Fill `count` values of n bytes each, value k at out[k*n], with synthetic
+ * generator `kind` (gibson_amd/csrc/synth.h) at indices first + k*stride.
+ * Bench/test data generation directly in HBM.
+ */
+int lzf_gpu_synth_fill(int kind, uint64_t seed, uint64_t first, uint64_t stride,
+                       uint32_t count, uint32_t n, uint8_t *out, void *stream);
+
+/*
+ * Host-memory batch (the north star's PCIe-inclusive path): the same as the
+ * device calls, but every pointer is host memory.  The library stages
+ * through pinned buffers and hipMemcpyAsync on its own stream and returns
+ * after the results are back in host memory.
+ */
+int lzf_host_compress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                            uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                            uint32_t *out_len, uint32_t count);
+int lzf_host_decompress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                              uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                              uint32_t *out_len, int32_t *err, uint32_t count);
+
+/* Which kernel generation the batch calls dispatch to (diagnostics):
+ * returns a static string such as "compress=window64 decompress=tokpar". */
+const char *lzf_gpu_kernel_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LZF_GPU_H */

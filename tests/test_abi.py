@@ -1,0 +1,70 @@
+"""The C-ABI boundary on CPU: the library builds, loads and exports every
+symbol include/*.h declares; no compute call is made without a GPU."""
+import ctypes
+import os
+import re
+
+from tests.oracle_lib import ROOT, sha16, synth
+
+import gibson_amd
+
+
+def _declared(header):
+    src = open(os.path.join(ROOT, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return set(re.findall(r"\b(lzf_\w+)\s*\(", src))
+
+
+def test_headers_declare_the_reference_pair():
+    # src/lzf.h:76-78, 95-97
+    assert _declared("lzf.h") == {"lzf_compress", "lzf_decompress"}
+    src = open(os.path.join(ROOT, "include", "lzf.h")).read()
+    assert re.search(r"#define\s+LZF_VERSION\s+0x0105", src)
+    assert 'extern "C"' in src
+
+
+def test_library_exports_every_declared_symbol():
+    L = gibson_amd.lib()
+    names = _declared("lzf.h") | _declared("lzf_gpu.h")
+    for n in sorted(names):
+        assert hasattr(L, n), n
+    assert set(gibson_amd.lzf.EXPORTS) <= names
+
+
+def test_library_is_gfx950_code_object():
+    data = open(gibson_amd.lib_path(), "rb").read()
+    assert b"gfx950" in data
+
+
+def test_no_cpu_codec_in_product_library():
+    # the product library must not contain (or link) the oracle
+    data = open(gibson_amd.lib_path(), "rb").read()
+    assert b"oracle_lzf" not in data
+    assert b"ref_lzf" not in data
+
+
+def test_version_constant():
+    assert gibson_amd.LZF_VERSION == 0x0105
+
+
+def test_host_generator_deterministic(golden):
+    seen = 0
+    for c in golden["compress"][:400]:
+        assert sha16(synth(c["kind"], c["seed"], c["index"], c["n"])) == c["in_sha"]
+        seen += 1
+    assert seen
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    import importlib
+    import gibson_amd.lzf as m
+    monkeypatch.setattr(m, "_LIB", None)
+    monkeypatch.setattr(m, "lib_path", lambda: str(tmp_path / "nope.so"))
+    try:
+        m.lib()
+    except m.LzfLibraryMissing:
+        pass
+    else:
+        raise AssertionError("missing library must raise")
+    finally:
+        importlib.reload(m)

@@ -1,0 +1,222 @@
+"""Parity of the HIP path with the oracle / golden vectors (needs a GPU).
+
+Everything here calls through the C-ABI of liblzf_hip.so: the drop-in pair
+(include/lzf.h) and the device batch API (include/lzf_gpu.h).  The bar is
+bit-exact: compressed streams, return values and errno are identical to the
+reference's (pinned by tests/golden and tests/test_oracle.py).
+"""
+import errno
+import os
+import random
+
+import numpy as np
+import pytest
+
+from tests.oracle_lib import sha16, synth
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+GENERATIONS = ["parallel", "serial"]
+
+
+@pytest.fixture(params=GENERATIONS)
+def generation(request, monkeypatch):
+    if request.param == "serial":
+        monkeypatch.setenv("LZF_GPU_KERNEL", "serial")
+    else:
+        monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    return request.param
+
+
+def _limit(gen):
+    # the serial generation keeps 16-bit positions
+    return 65536 if gen == "serial" else 1 << 30
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import gibson_amd
+    gibson_amd.lib()
+
+
+def test_kernel_info_names_native_path():
+    import gibson_amd
+    info = gibson_amd.kernel_info()
+    assert "compress=" in info and "decompress=" in info
+
+
+def test_single_call_dropin_kat(kat):
+    import gibson_amd
+    for c in kat:
+        data = bytes.fromhex(c["in_hex"])
+        if c["op"] == "compress":
+            r = gibson_amd.lzf_compress(data, c["out_len"])
+            assert (len(r) if r else 0) == c["result"], c
+            if r:
+                assert r.hex() == c["out_hex"]
+        else:
+            out, e = gibson_amd.lzf_decompress(data, c["out_len"])
+            assert (len(out) if out else 0) == c["result"], c
+            assert e == c["errno"], c
+            if out:
+                assert out.hex() == c["out_hex"]
+
+
+def test_batch_compress_golden(golden, generation):
+    from tests.gpu_batch import gpu_compress
+    cases = [c for c in golden["compress"] if c["n"] <= _limit(generation)]
+    inputs = {}
+    for c in cases:
+        key = (c["kind"], c["seed"], c["index"], c["n"])
+        if key not in inputs:
+            inputs[key] = synth(*key)
+    vals = [inputs[(c["kind"], c["seed"], c["index"], c["n"])] for c in cases]
+    caps = [c["out_len"] for c in cases]
+    res = gpu_compress(vals, caps)
+    bad = []
+    for c, r in zip(cases, res):
+        if (len(r) if r else 0) != c["result"] or (r and sha16(r) != c["out_sha"]):
+            bad.append((c["kind"], c["n"], c["out_len"], c["result"], len(r) if r else 0))
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:5]}"
+
+
+def test_batch_decompress_golden(golden, oracle):
+    from tests.gpu_batch import gpu_decompress
+    from tests.test_oracle import decoder_cases
+    cases = list(decoder_cases(golden, oracle))
+    res = gpu_decompress([s for _, s in cases], [c["out_len"] for c, _ in cases])
+    bad = []
+    for (c, s), (out, e) in zip(cases, res):
+        if (len(out) if out else 0) != c["result"] or e != c["errno"] or \
+                (out and sha16(out) != c["out_sha"]):
+            bad.append((c.get("tag"), c["n"] if "n" in c else None, c["result"], c["errno"],
+                        len(out) if out else 0, e))
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:5]}"
+
+
+def test_batch_decompress_serial_generation(golden, oracle, monkeypatch):
+    monkeypatch.setenv("LZF_GPU_KERNEL", "serial")
+    test_batch_decompress_golden(golden, oracle)
+
+
+def test_random_differential(oracle, generation):
+    from tests.gpu_batch import gpu_compress, gpu_decompress
+    rnd = random.Random(7)
+    vals, caps = [], []
+    for it in range(3000):
+        kind = rnd.randrange(6)
+        n = rnd.choice([rnd.randint(1, 64), rnd.randint(1, 700), rnd.randint(1, 9000)])
+        v = synth(kind, rnd.getrandbits(32), it, n)
+        if rnd.random() < 0.2:
+            v = bytes(rnd.choice(b"ab") for _ in range(n))
+        vals.append(v)
+        caps.append(rnd.choice([max(1, n - 4), n + n // 16 + 64, rnd.randint(1, n + 64)]))
+    res = gpu_compress(vals, caps)
+    exp = [oracle.compress(v, c) for v, c in zip(vals, caps)]
+    bad = [i for i, (a, b) in enumerate(zip(res, exp)) if a != b]
+    assert not bad, f"{len(bad)} mismatches; first {bad[:5]}"
+    streams = [r for r in exp if r]
+    origs = [v for v, r in zip(vals, exp) if r]
+    dec = gpu_decompress(streams, [len(v) for v in origs])
+    assert all(d == (v, 0) for d, v in zip(dec, origs))
+
+
+def test_edge_cases(oracle):
+    from tests.gpu_batch import gpu_compress, gpu_decompress
+    vals = [b"", b"x", b"x", b"ab", b"abc", b"a" * 5, b"a" * 300, b"\0" * 65536,
+            bytes(range(256)) * 4, b"ab" * 4000]
+    caps = [10, 3, 4, 5, 6, 1, 296, 65532, 1020, 8000]
+    res = gpu_compress(vals, caps)
+    for v, c, r in zip(vals, caps, res):
+        assert r == oracle.compress(v, c), (len(v), c)
+    streams = [b"", b"\x00", b"\xe0\x00\x00", b"\x1f" + b"q" * 31, b"\x00z\xa0\x00"]
+    for cap in (0, 1, 7, 8, 32, 4096):
+        dec = gpu_decompress(streams, [cap] * len(streams))
+        for s, d in zip(streams, dec):
+            # phantom control byte 0xff for the empty stream, as in tests/golden
+            o, e = oracle.decompress(s, cap)
+            assert d == (o, e), (s, cap, d, (o, e))
+
+
+def test_device_generator_matches_host():
+    import gibson_amd
+    for kind in range(6):
+        for n in (1, 37, 4096, 16384):
+            out = torch.zeros(3 * n, dtype=torch.uint8, device="cuda")
+            gibson_amd.synth_fill(kind, 0x5EED0002, 5, 7, 3, n, out)
+            torch.cuda.synchronize()
+            host = b"".join(synth(kind, 0x5EED0002, 5 + 7 * k, n) for k in range(3))
+            assert bytes(out.cpu().numpy()) == host, (kind, n)
+
+
+# ---- BASELINE.json sizes: size-independent properties + sampled oracle ----
+
+CONFIGS = [
+    # (kind, seed, n, count) -- scaled batches of configs 2..5
+    (1, 0x5EED0002, 4096, 65536),
+    (2, 0x5EED0003, 65536, 2048),
+    (0, 0x5EED0004, 8192, 16384),
+    (3, 0x5EED0005, 16384, 8192),
+]
+
+
+@pytest.mark.parametrize("kind,seed,n,count", CONFIGS)
+def test_full_size_roundtrip(kind, seed, n, count, oracle):
+    import gibson_amd
+    dev = "cuda"
+    src = torch.empty(count * n, dtype=torch.uint8, device=dev)
+    gibson_amd.synth_fill(kind, seed, 0, 1, count, n, src)
+    in_off = torch.arange(count, dtype=torch.int64, device=dev) * n
+    in_len = torch.full((count,), n, dtype=torch.int32, device=dev)
+    cap = torch.full((count,), n - 4, dtype=torch.int32, device=dev)
+    comp = torch.zeros(count * n, dtype=torch.uint8, device=dev)
+    clen = torch.zeros(count, dtype=torch.int32, device=dev)
+    gibson_amd.compress_batch(src, in_off, in_len, comp, in_off, cap, clen, n)
+    dec = torch.zeros(count * n, dtype=torch.uint8, device=dev)
+    dlen = torch.zeros(count, dtype=torch.int32, device=dev)
+    err = torch.zeros(count, dtype=torch.int32, device=dev)
+    ok = clen > 0
+    dcap = torch.where(ok, torch.full_like(clen, n), torch.zeros_like(clen))
+    gibson_amd.decompress_batch(comp, in_off, torch.where(ok, clen, torch.ones_like(clen)),
+                                dec, in_off, dcap, dlen, err, n)
+    torch.cuda.synchronize()
+    # round trip identity on every compressed value
+    assert torch.equal(dlen[ok], torch.full_like(dlen[ok], n))
+    okm = ok.repeat_interleave(n)
+    assert torch.equal(dec[okm], src[okm])
+    assert int(ok.sum()) > 0
+    # bit-exact vs the oracle on a sample (incl. the failures)
+    rnd = random.Random(kind)
+    cl = clen.cpu().numpy()
+    sample = rnd.sample(range(count), 48)
+    host_src = src.view(count, n)[sample].cpu().numpy()
+    host_cmp = comp.view(count, n)[sample].cpu().numpy()
+    for k, i in enumerate(sample):
+        exp = oracle.compress(bytes(host_src[k]), n - 4)
+        got = bytes(host_cmp[k][:cl[i]]) if cl[i] else None
+        assert got == exp, (kind, n, i)
+
+
+def test_host_batch_api(oracle):
+    import gibson_amd
+    vals = [synth(1, 11, i, 4096) for i in range(64)] + [synth(4, 11, 0, 4096)]
+    arena = np.frombuffer(b"".join(vals), np.uint8).copy()
+    off = np.arange(len(vals), dtype=np.uint64) * 4096
+    ln = np.full(len(vals), 4096, np.uint32)
+    cap = np.full(len(vals), 4092, np.uint32)
+    out = np.zeros_like(arena)
+    olen = np.zeros(len(vals), np.uint32)
+    gibson_amd.host_compress_batch(arena, off, ln, out, off, cap, olen)
+    for i, v in enumerate(vals):
+        exp = oracle.compress(v, 4092)
+        got = bytes(out[off[i]:off[i] + olen[i]]) if olen[i] else None
+        assert got == exp
+    dec = np.zeros_like(arena)
+    dl = np.zeros(len(vals), np.uint32)
+    er = np.zeros(len(vals), np.int32)
+    ok = olen > 0
+    gibson_amd.host_decompress_batch(out, off[ok], olen[ok], dec, off[ok], ln[ok], dl, er)
+    assert (dl[:ok.sum()] == 4096).all() and (er[:ok.sum()] == 0).all()

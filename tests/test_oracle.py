@@ -1,0 +1,101 @@
+"""The CPU oracle against the reference's golden vectors (CPU only).
+
+Pins oracle/lzf_oracle.c to the reference codec before it is trusted as the
+checker of the HIP path: known answers, the randomized
+corpus generated from the compiled reference (tests/golden/make_golden.py),
+and -- where oracle/_ref was built in this container -- a live differential
+run against the reference itself.
+"""
+import random
+
+import pytest
+
+from tests import oracle_lib
+from tests.oracle_lib import sha16, synth
+
+
+def test_kat(kat, oracle):
+    for c in kat:
+        data = bytes.fromhex(c["in_hex"])
+        if c["op"] == "compress":
+            r = oracle.compress(data, c["out_len"])
+            assert (len(r) if r else 0) == c["result"], c
+            if r:
+                assert r.hex() == c["out_hex"], c
+        else:
+            out, e = oracle.decompress(data, c["out_len"])
+            assert (len(out) if out else 0) == c["result"], c
+            assert e == c["errno"], c
+            if out:
+                assert out.hex() == c["out_hex"], c
+
+
+def test_quirk_19_byte_ref(oracle):
+    # "Z"+X19+X19 emits a 19-byte ref e0 0a 12
+    data = b"Z" + b"abcdefghijklmnopqrs" * 2
+    assert oracle.compress(data, 1000).endswith(bytes.fromhex("e00a12"))
+
+
+def test_corpus_compress(golden, oracle):
+    cache = {}
+    for c in golden["compress"]:
+        key = (c["kind"], c["seed"], c["index"], c["n"])
+        if key not in cache:
+            cache[key] = synth(*key)
+        data = cache[key]
+        assert sha16(data) == c["in_sha"], "synthetic generator drifted"
+        r = oracle.compress(data, c["out_len"])
+        assert (len(r) if r else 0) == c["result"], c
+        if r:
+            assert sha16(r) == c["out_sha"], c
+            if "out_hex" in c:
+                assert r.hex() == c["out_hex"]
+
+
+def _stream_for(c, oracle):
+    data = synth(c["kind"], c["seed"], c["index"], c["n"])
+    n = c["n"]
+    stream = oracle.compress(data, n + n // 16 + 64)
+    assert len(stream) == c["stream_len"] and sha16(stream) == c["stream_sha"]
+    if "cut" in c:
+        stream = stream[:c["cut"]]
+    if "flip" in c:
+        b = bytearray(stream)
+        b[c["flip"][0]] = c["flip"][1]
+        stream = bytes(b)
+    return stream
+
+
+def decoder_cases(golden, oracle):
+    for c in golden["decompress"]:
+        s = bytes.fromhex(c["in_hex"]) if "in_hex" in c else _stream_for(c, oracle)
+        yield c, s
+
+
+def test_corpus_decompress(golden, oracle):
+    for c, s in decoder_cases(golden, oracle):
+        out, e = oracle.decompress(s, c["out_len"])
+        assert (len(out) if out else 0) == c["result"], c
+        assert e == c["errno"], c
+        if out:
+            assert sha16(out) == c["out_sha"], c
+
+
+@pytest.mark.skipif(oracle_lib.reference() is None, reason="oracle/_ref not built here")
+def test_differential_vs_reference(oracle):
+    ref = oracle_lib.reference()
+    rnd = random.Random(1234)
+    for it in range(3000):
+        kind = rnd.randrange(6)
+        n = rnd.choice([rnd.randint(1, 64), rnd.randint(1, 600), rnd.randint(1, 5000)])
+        data = synth(kind, rnd.getrandbits(32), it, n)
+        for out_len in (max(1, n - 4), n + 40, rnd.randint(1, n + 40)):
+            assert oracle.compress(data, out_len) == ref.compress(data, out_len)
+        s = ref.compress(data, n + n // 16 + 64)
+        for out_len in (n, n - 1, rnd.randint(0, n + 5)):
+            assert oracle.decompress(s, out_len) == ref.decompress(s, out_len)
+        if len(s) > 2:
+            b = bytearray(s)
+            b[rnd.randrange(len(b))] = rnd.randrange(256)
+            b = bytes(b[:rnd.randint(0, len(b))])
+            assert oracle.decompress(b, n + 10) == ref.decompress(b, n + 10)
