@@ -166,9 +166,12 @@ def main():
     n_ok = int(ok.sum())
     c_bytes = int(clen.to(torch.int64).sum())
     # sanity (outside the timed region): every compressed value decoded back
-    good = bool(torch.equal(dlen[ok], torch.full_like(dlen[ok], n)))
-    okm = ok.repeat_interleave(n)
-    good = good and bool(torch.equal(dec[okm], src[okm]))
+    good = bool(((dlen == n) | ~ok).all())
+    dv, sv = dec.view(count, n), src.view(count, n)
+    for r0 in range(0, count, 1 << 16):
+        r1 = min(count, r0 + (1 << 16))
+        diff = (dv[r0:r1] != sv[r0:r1]).any(dim=1) & ok[r0:r1]
+        good = good and not bool(diff.any())
 
     stats = torch.tensor([wall, t_comp, t_dec], dtype=torch.float64, device=dev)
     tot = torch.tensor([count * n, n_ok, c_bytes, 0 if good else 1], dtype=torch.float64,

@@ -43,7 +43,8 @@ def lib():
     global _LIB
     if _LIB is not None:
         return _LIB
-    path = lib_path()
+    # LZF_HIP_LIB: load a diagnostic build (e.g. liblzf_hip_stats.so) instead
+    path = os.environ.get("LZF_HIP_LIB") or lib_path()
     if not os.path.exists(path):
         raise LzfLibraryMissing(f"{path} not built: run __graft_entry__.build() "
                                 "(make -C gibson_amd/csrc); there is no CPU fallback")
