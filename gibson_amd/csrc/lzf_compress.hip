@@ -8,31 +8,34 @@
  * exact semantics but resolves it 64 positions ("a window") at a time:
  *
  *   1. every lane i takes position p = P+i: slot(p) (src/lzf_c.c:47-57) and
- *      the nearest earlier lane with the same slot (prevW), found through a
- *      256-key LDS bitmask (ds_or_b64) -- the ref IF every window position
- *      were inserted;
- *   2. lanes without prevW look the slot up in the exact table of inserted
- *      positions < P: 4096 bucket heads + a skip chain over the last 8192
- *      positions (entry = slot << 16 | distance to the latest earlier
- *      inserted position of the bucket with a DIFFERENT slot).  The walk
- *      stops at the first entry with the same 16-bit slot -- exactly the
- *      pointer the reference's 65536-slot table holds -- or beyond the 8 KiB
- *      window, where the reference's `off < MAX_OFF` test fails too;
+ *      the exact sets of window lanes sharing its slot / its head bucket,
+ *      from three small LDS lane bitmaps keyed by bits 0-5, 6-11, 12-15 of
+ *      a bijective slot mix (ds_or_b64; same slot = all three agree, same
+ *      bucket = bits 6-15 agree).  The nearest earlier same-slot lane (prevW) is the ref IF
+ *      every window position were inserted;
+ *   2. every lane also looks the slot up in the exact table of inserted
+ *      positions < P: 1024 bucket heads (slot, pos) + a skip chain over the
+ *      last 8192 positions (distance to the latest earlier inserted position
+ *      of the bucket with a DIFFERENT slot).  The walk stops at the first
+ *      entry with the same 16-bit slot -- exactly the pointer the
+ *      reference's 65536-slot table holds -- or beyond the 8 KiB window,
+ *      where the reference's `off < MAX_OFF` test fails too;
  *   3. match test and length per lane (src/lzf_c.c:151-209, including the 16
  *      unconditional compares: lim = maxlen>16 ? max(maxlen,19) : maxlen),
  *      probed up to 11 bytes per lane;
  *   4. the parse orbit: a minimal scalar loop over match lanes (s_ff1 on the
  *      ballot); a match on the orbit that reached the probe cap gets its
- *      exact length from a whole-wave 256-byte compare;
- *   5. validation: a visited lane whose prevW lies inside a match (not
- *      inserted by the reference, src/lzf_c.c:227-247) would have read an
- *      older entry -- the window is accepted up to that lane only;
- *   6. emission: the reference's output cursor (reserved run header,
+ *      exact length from a whole-wave 256-byte compare.  A visited lane
+ *      whose prevW lies inside an earlier match (not inserted by the
+ *      reference, src/lzf_c.c:227-247) is repaired in place: its ref becomes
+ *      the latest inserted same-slot lane, else the table entry from step 2;
+ *   5. emission: the reference's output cursor (reserved run header,
  *      32-literal rollover, undo of an empty run, out-of-space checks at
  *      src/lzf_c.c:176, 263, 276) is a function of per-lane run indices and
  *      one wave prefix sum (DPP) of per-token sizes; all lanes store their
  *      literal / header / back-reference bytes in parallel;
- *   7. the window's inserted positions go into heads / skip chain.
+ *   6. the window's inserted positions go into heads / skip chain, the last
+ *      one per bucket and each one's skip target read off the lane bitmaps.
  *
  * Nothing is ever written at or past out_cap; the return value (0 or the
  * stream length) and the stream are identical to the reference's.
@@ -40,11 +43,11 @@
 #include "lzf_internal.h"
 
 #define CW_LANES     64u
-#define CW_HBUCKETS  4096u
-#define CW_KEYS      256u
+#define CW_HBITS     10
+#define CW_HBUCKETS  (1u << CW_HBITS)
 #define CW_CHAIN     8192u
 #define CW_RING_MAX  16384u
-#define CW_EXT_CAP   11u          /* per-lane match length probe (3 + 2 x 4 bytes) */
+#define CW_EXT_CAP   19u          /* per-lane match length probe (3 + 4 x 4 bytes) */
 
 /* Diagnostic build only (make stats -> liblzf_hip_stats.so): per-phase
  * s_memtime cycles and event counts, summed over all waves. */
@@ -79,11 +82,6 @@ __device__ __forceinline__ uint32_t slot_of(uint32_t tri)
     return (((b0 << 8) | b1) - 5u * ((b1 << 8) | b2)) & 0xFFFFu;
 }
 
-__device__ __forceinline__ uint32_t hbucket(uint32_t slot)
-{
-    return ((slot * 40503u) >> 4) & (CW_HBUCKETS - 1u);
-}
-
 /* Order-preserving LDS hand-off between the lanes of the (single-wave)
  * workgroup: LDS ops of one wave execute in order, so only the compiler
  * must not move memory operations across this point. */
@@ -105,15 +103,36 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x)
     return x;
 }
 
+/* Bucket-head entry: slot and position of the latest inserted position of
+ * the bucket.  Values up to 64 KiB pack both into 32 bits. */
+template <typename E> struct HeadOps;
+template <> struct HeadOps<uint32_t> {
+    static constexpr uint32_t NONE = 0xFFFFFFFFu;
+    __device__ static uint32_t make(uint32_t s, uint32_t p) { return (s << 16) | (p & 0xFFFFu); }
+    __device__ static uint32_t pos(uint32_t e) { return e & 0xFFFFu; }
+    __device__ static uint32_t slot(uint32_t e) { return e >> 16; }
+};
+template <> struct HeadOps<unsigned long long> {
+    static constexpr unsigned long long NONE = ~0ull;
+    __device__ static unsigned long long make(uint32_t s, uint32_t p)
+    {
+        return ((unsigned long long)s << 32) | p;
+    }
+    __device__ static uint32_t pos(unsigned long long e) { return (uint32_t)e; }
+    __device__ static uint32_t slot(unsigned long long e) { return (uint32_t)(e >> 32); }
+};
+
 template <typename HeadT>
 struct CwLds {
     uint8_t *ring;        /* input ring, R bytes (power of two) */
     uint32_t rmask;       /* R - 1 */
-    HeadT *head;          /* CW_HBUCKETS: latest inserted position of the bucket */
-    uint32_t *chain;      /* per inserted position: slot << 16 | skip distance */
+    HeadT *head;          /* CW_HBUCKETS: latest inserted (slot, pos) of the bucket */
+    uint16_t *chain;      /* per inserted position: distance to the latest earlier
+                           * inserted position of its bucket with another slot */
     uint32_t cmask;       /* chain ring entries - 1 */
-    unsigned long long *keymask; /* CW_KEYS: window lanes per bucket key */
-    uint32_t *sb;         /* 64 x (bucket << 16 | slot) of the window */
+    unsigned long long *t1, *t2, *t3;   /* window lane bitmaps keyed by slot-mix bits
+                                         * 0-5, 6-11, 12-15 */
+    uint32_t *flag;       /* 64 orbit flags */
 
     __device__ __forceinline__ uint32_t rd4(uint32_t x) const
     {
@@ -148,36 +167,86 @@ __device__ void cw_fill(const CwLds<HeadT> &L, const uint8_t *src, uint32_t from
     }
 }
 
+__device__ __forceinline__ uint32_t slot_mix(uint32_t s) { return (s * 40503u) & 0xFFFFu; }
+__device__ __forceinline__ uint32_t bucket_of(uint32_t sm) { return sm >> (16 - CW_HBITS); }
+
 /* Insert position x (slot sx) after every earlier position (one lane). */
 template <typename HeadT>
 __device__ __forceinline__ void cw_insert_one(const CwLds<HeadT> &L, uint32_t x, uint32_t sx)
 {
-    const HeadT NONE = (HeadT)~(HeadT)0;
-    uint32_t bx = hbucket(sx);
-    uint32_t h = (uint32_t)L.head[bx];
+    typedef HeadOps<HeadT> H;
+    const uint32_t bx = bucket_of(slot_mix(sx));
+    const HeadT hv = L.head[bx];
     uint32_t y = 0xFFFFFFFFu;
-    if (h != (uint32_t)NONE && x - h <= LZF_WINDOW) {
-        uint32_t eh = L.chain[h & L.cmask];
-        if ((eh >> 16) != sx) y = h;
-        else if (eh & 0xFFFFu) y = h - (eh & 0xFFFFu);
+    if (hv != H::NONE && x - H::pos(hv) <= LZF_WINDOW) {
+        const uint32_t hp = H::pos(hv);
+        if (H::slot(hv) != sx) y = hp;
+        else if (L.chain[hp & L.cmask]) y = hp - L.chain[hp & L.cmask];
     }
-    L.chain[x & L.cmask] = (sx << 16) | ((y != 0xFFFFFFFFu && x - y <= LZF_WINDOW) ? x - y : 0u);
-    L.head[bx] = (HeadT)x;
+    L.chain[x & L.cmask] = (uint16_t)((y != 0xFFFFFFFFu && x - y <= LZF_WINDOW) ? x - y : 0u);
+    L.head[bx] = H::make(sx, x);
+}
+
+/* Length of the match p/r whose first k0 bytes are known equal, up to lim:
+ * the whole wave compares 256 bytes per step (uniform inputs and result). */
+template <typename HeadT>
+__device__ __forceinline__ uint32_t cw_coop_len(const CwLds<HeadT> &L, uint32_t p, uint32_t r,
+                                                uint32_t k0, uint32_t lim)
+{
+    const uint32_t lane = threadIdx.x;
+    uint32_t kb = k0;
+    while (kb < lim) {
+        const uint32_t kk = kb + 4u * lane;
+        uint32_t x = 0;
+        if (kk < lim) {
+            x = L.rd4(p + kk) ^ L.rd4(r + kk);
+            const uint32_t rem = lim - kk;
+            if (rem < 4u) x |= 0xFFFFFFFFu << (8u * rem);
+        }
+        const uint64_t hit = __ballot(x != 0u);
+        if (hit) {
+            const uint32_t fl = (uint32_t)__builtin_ctzll(hit);
+            const uint32_t xf = __builtin_amdgcn_readlane(x, fl);
+            const uint32_t k = kb + 4u * fl + ((uint32_t)__builtin_ctz(xf) >> 3);
+            return k < lim ? k : lim;
+        }
+        kb += 4u * CW_LANES;
+    }
+    return lim;
+}
+
+__device__ __forceinline__ uint32_t match_lim(uint32_t n, uint32_t p)
+{
+    uint32_t maxlen = n - p - 2u;
+    if (maxlen > LZF_MAX_REF) maxlen = LZF_MAX_REF;
+    return (maxlen > 16u && maxlen < 19u) ? 19u : maxlen;   /* src/lzf_c.c:181-206 */
+}
+
+__device__ __forceinline__ uint32_t readlane_u32(uint32_t v, uint32_t l)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, uint32_t l)
+{
+    return ((uint64_t)readlane_u32((uint32_t)(v >> 32), l) << 32) | readlane_u32((uint32_t)v, l);
 }
 
 template <typename HeadT>
 __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, uint32_t ring_bytes)
 {
+    typedef HeadOps<HeadT> H;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const HeadT NONE = (HeadT)~(HeadT)0;
     CwLds<HeadT> L;
     L.ring = smem;
     L.rmask = ring_bytes - 1u;
     uint8_t *cur = smem + ring_bytes;
-    L.keymask = (unsigned long long *)cur;  cur += CW_KEYS * 8u;
-    L.sb = (uint32_t *)cur;                 cur += CW_LANES * 4u;
-    L.head = (HeadT *)cur;                  cur += CW_HBUCKETS * sizeof(HeadT);
-    L.chain = (uint32_t *)cur;
+    L.head = (HeadT *)cur;                   cur += CW_HBUCKETS * sizeof(HeadT);
+    L.t1 = (unsigned long long *)cur;        cur += 64u * 8u;
+    L.t2 = (unsigned long long *)cur;        cur += 64u * 8u;
+    L.t3 = (unsigned long long *)cur;        cur += 16u * 8u;
+    L.flag = (uint32_t *)cur;                cur += CW_LANES * 4u;
+    L.chain = (uint16_t *)cur;
     L.cmask = (ring_bytes < CW_CHAIN ? ring_bytes : CW_CHAIN) - 1u;
 
     const uint32_t lane = threadIdx.x;
@@ -197,10 +266,11 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
         return;
     }
 
-    for (uint32_t k = lane; k < CW_KEYS; k += CW_LANES) L.keymask[k] = 0ull;
     {
-        uint32_t *h32 = (uint32_t *)L.head;
-        for (uint32_t k = lane; k < CW_HBUCKETS * sizeof(HeadT) / 4u; k += CW_LANES) h32[k] = ~0u;
+        uint32_t *z = (uint32_t *)L.head;   /* heads = NONE, bitmaps = 0 */
+        const uint32_t nh = CW_HBUCKETS * sizeof(HeadT) / 4u;
+        for (uint32_t k = lane; k < nh; k += CW_LANES) z[k] = ~0u;
+        for (uint32_t k = lane; k < (64u + 64u + 16u) * 2u; k += CW_LANES) z[nh + k] = 0u;
     }
     uint32_t loaded = n < ring_bytes ? n : ring_bytes;
     cw_fill(L, src, 0u, loaded);
@@ -228,64 +298,72 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
         CW_PHASE(1);
         CW_STAT_ADD(windows, 1);
 
+        /* ---- 1. slots and same-slot / same-bucket lane sets ---------- */
         const uint32_t lim_lane = (n - 2u - P) < CW_LANES ? (n - 2u - P) : CW_LANES;
         const uint32_t p = P + lane;
         const bool valid = lane < lim_lane;
         const uint32_t tri = L.rd4(p) & 0xFFFFFFu;
-        const uint32_t s = valid ? slot_of(tri) : 0xFFFFFFFFu;
-        const uint32_t b = valid ? hbucket(s) : 0u;
-        const uint32_t key = b & (CW_KEYS - 1u);
-        L.sb[lane] = (b << 16) | (s & 0xFFFFu);
-        if (valid) atomicOr(&L.keymask[key], 1ull << lane);
+        const uint32_t s = slot_of(tri);
+        const uint32_t sm = slot_mix(s);          /* bijective 16-bit mix of the slot */
+        const uint32_t b = bucket_of(sm);
+        const uint32_t k1 = sm & 63u, k2 = (sm >> 6) & 63u, k3 = sm >> 12;
+        const unsigned long long me = 1ull << lane;
+        if (valid) {
+            atomicOr(&L.t1[k1], me);
+            atomicOr(&L.t2[k2], me);
+            atomicOr(&L.t3[k3], me);
+        }
         wave_lds_fence();
-        const uint64_t M = valid ? L.keymask[key] : 0ull;
-        const uint32_t head_old = valid ? (uint32_t)L.head[b] : (uint32_t)NONE;
+        uint64_t M1 = 0, M2 = 0, M3 = 0;
+        HeadT hv = H::NONE;
+        if (valid) {
+            M1 = L.t1[k1];
+            M2 = L.t2[k2];
+            M3 = L.t3[k3];
+            hv = L.head[b];
+        }
         wave_lds_fence();
-        if (valid) L.keymask[key] = 0ull;
+        if (valid) {
+            L.t1[k1] = 0ull;
+            L.t2[k2] = 0ull;
+            L.t3[k3] = 0ull;
+        }
+        const uint64_t Mb = M2 & M3;              /* lanes with my bucket (mix bits 6-15) */
+        const uint64_t Ms = M1 & Mb;              /* lanes with my slot (all 16 bits) */
+        const uint64_t msb = Ms & lanemask_lt(lane);
+        int prevW = msb ? (int)(63u - (uint32_t)__builtin_clzll(msb)) : -1;
         CW_PHASE(2);
 
-        /* 1. nearest earlier window lane with the same slot */
-        int prevW = -1;
-        for (uint64_t cand = M & lanemask_lt(lane); cand;) {
-            uint32_t j = 63u - __builtin_clzll(cand);
-            cand &= ~(1ull << j);
-            if ((L.sb[j] & 0xFFFFu) == s) { prevW = (int)j; break; }
+        /* ---- 2. exact table lookup among positions < P (all lanes) ---- */
+        uint32_t T = 0xFFFFFFFFu;
+        if (valid && hv != H::NONE) {
+            uint32_t q = H::pos(hv), sq = H::slot(hv);
+            while (p - q <= LZF_WINDOW) {
+                if (sq == s) { T = q; break; }
+                CW_STAT_ADD(hops, 1);
+                const uint32_t d = L.chain[q & L.cmask];   /* skip q's run of its slot */
+                if (d == 0u) break;
+                q -= d;
+                sq = slot_of(L.rd4(q) & 0xFFFFFFu);
+            }
         }
         CW_PHASE(3);
 
-        /* 2. exact table lookup for positions < P */
-        uint32_t ref = 0xFFFFFFFFu;
-        if (prevW >= 0) {
-            ref = P + (uint32_t)prevW;
-        } else if (head_old != (uint32_t)NONE) {
-            uint32_t q = head_old;
-            while (p - q <= LZF_WINDOW) {
-                CW_STAT_ADD(hops, 1);
-                uint32_t e = L.chain[q & L.cmask];
-                if ((e >> 16) == s) { ref = q; break; }
-                uint32_t d = e & 0xFFFFu;     /* skip q's whole run of its slot */
-                if (d == 0u) break;
-                q -= d;
-            }
-        }
-        CW_PHASE(4);
-
-        /* 3. match test (src/lzf_c.c:151-166) and probed length (169-209) */
+        /* ---- 3. match test (src/lzf_c.c:151-166), probed length ------ */
+        uint32_t ref = prevW >= 0 ? P + (uint32_t)prevW : T;
         const bool match = valid && ref != 0xFFFFFFFFu && ref > 0u &&
                            (p - ref - 1u) < LZF_WINDOW && p + 4u < n &&
                            (L.rd4(ref) & 0xFFFFFFu) == tri;
         uint32_t lim = 0, m = 1;
         bool exact = true;
         if (match) {
-            uint32_t maxlen = n - p - 2u;
-            if (maxlen > LZF_MAX_REF) maxlen = LZF_MAX_REF;
-            lim = (maxlen > 16u && maxlen < 19u) ? 19u : maxlen;
+            lim = match_lim(n, p);
             const uint32_t kc = lim < CW_EXT_CAP ? lim : CW_EXT_CAP;
             uint32_t k = 3u;
             while (k < kc) {
                 CW_STAT_ADD(ext, 1);
                 uint32_t x = L.rd4(p + k) ^ L.rd4(ref + k);
-                uint32_t rem = kc - k;
+                const uint32_t rem = kc - k;
                 if (rem < 4u) x |= 0xFFFFFFFFu << (8u * rem);
                 if (x) { k += (uint32_t)__builtin_ctz(x) >> 3; break; }
                 k += 4u;
@@ -293,80 +371,97 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
             m = k < kc ? k : kc;
             exact = (m < kc) || (kc == lim);
         }
-        CW_PHASE(5);
+        CW_PHASE(4);
 
-        /* 4. the parse orbit: one scalar step per match on it */
-        const uint64_t MM = __ballot(match) & lanemask_lt(lim_lane);
-        const uint64_t NX = __ballot(!exact);
-        uint64_t V = 0, MMV = 0;
-        uint32_t i0 = 0, end = lim_lane, mexit = 0;
+        /* ---- 4. the parse orbit -----------------------------------------
+         * Pointer doubling: nxt(i) = i+1 (literal) or i+m (match), J_k =
+         * nxt^(2^k); lane t computes J^t(s0) and flags that lane, so one
+         * pass yields every visited lane from s0 on.  A pass stops at a match
+         * whose length is still only a lower bound (resolved by a whole-wave
+         * compare) and is redone from a lane whose speculative ref was not
+         * inserted (repaired in place, see step 4 in the header). */
+        uint64_t MMc = __ballot(match) & lanemask_lt(lim_lane);
+        uint64_t NXc = __ballot(!exact) & MMc;
+        uint64_t V = 0;
+        uint32_t s0 = 0, end = lim_lane, mexit = 0;
         int exitLane = -1;
         for (;;) {
-            const uint64_t rest = MM & ~lanemask_lt(i0);
-            if (!rest) {
-                V |= range_mask(i0, lim_lane);
-                break;
-            }
-            const uint32_t j = (uint32_t)__builtin_ctzll(rest);
-            V |= range_mask(i0, j + 1u);
-            MMV |= 1ull << j;
-            uint32_t mj = __builtin_amdgcn_readlane(m, j);
-            if ((NX >> j) & 1ull) {
-                /* exact length of a long match on the orbit, 256 B per step */
+            /* one doubling pass from s0 */
+            const bool mine_m = (MMc >> lane) & 1ull;
+            uint32_t nx = lane + (mine_m ? m : 1u);
+            if (lane >= lim_lane || nx > CW_LANES || ((NXc >> lane) & 1ull)) nx = CW_LANES;
+            uint32_t J0 = nx, J1, J2, J3, J4, J5;
+            J1 = J0 >= CW_LANES ? CW_LANES : (uint32_t)__shfl((int)J0, (int)J0);
+            J2 = J1 >= CW_LANES ? CW_LANES : (uint32_t)__shfl((int)J1, (int)J1);
+            J3 = J2 >= CW_LANES ? CW_LANES : (uint32_t)__shfl((int)J2, (int)J2);
+            J4 = J3 >= CW_LANES ? CW_LANES : (uint32_t)__shfl((int)J3, (int)J3);
+            J5 = J4 >= CW_LANES ? CW_LANES : (uint32_t)__shfl((int)J4, (int)J4);
+            uint32_t x = s0, y;
+            y = (uint32_t)__shfl((int)J0, (int)(x & 63u)); if ((lane & 1u) && x < CW_LANES) x = y;
+            y = (uint32_t)__shfl((int)J1, (int)(x & 63u)); if ((lane & 2u) && x < CW_LANES) x = y;
+            y = (uint32_t)__shfl((int)J2, (int)(x & 63u)); if ((lane & 4u) && x < CW_LANES) x = y;
+            y = (uint32_t)__shfl((int)J3, (int)(x & 63u)); if ((lane & 8u) && x < CW_LANES) x = y;
+            y = (uint32_t)__shfl((int)J4, (int)(x & 63u)); if ((lane & 16u) && x < CW_LANES) x = y;
+            y = (uint32_t)__shfl((int)J5, (int)(x & 63u)); if ((lane & 32u) && x < CW_LANES) x = y;
+            L.flag[lane] = 0u;
+            wave_lds_fence();
+            if (x < CW_LANES) L.flag[x] = 1u;
+            wave_lds_fence();
+            const uint64_t Vp = __ballot(L.flag[lane] != 0u) & lanemask_lt(lim_lane);
+            V = (V & lanemask_lt(s0)) | Vp;
+            const uint32_t last = 63u - (uint32_t)__builtin_clzll(V);
+            if ((NXc >> last) & 1ull) {
+                /* a long match on the orbit: exact length, 256 B per step */
                 CW_STAT_ADD(coop, 1);
-                const uint32_t pj = P + j;
-                const uint32_t rj = __builtin_amdgcn_readlane(ref, j);
-                const uint32_t limj = __builtin_amdgcn_readlane(lim, j);
-                uint32_t kb = mj;
-                mj = limj;
-                while (kb < limj) {
-                    const uint32_t kk = kb + 4u * lane;
-                    uint32_t x = 0;
-                    if (kk < limj) {
-                        x = L.rd4(pj + kk) ^ L.rd4(rj + kk);
-                        const uint32_t rem = limj - kk;
-                        if (rem < 4u) x |= 0xFFFFFFFFu << (8u * rem);
-                    }
-                    const uint64_t hit = __ballot(x != 0u);
-                    if (hit) {
-                        const uint32_t fl = (uint32_t)__builtin_ctzll(hit);
-                        const uint32_t xf = __builtin_amdgcn_readlane(x, fl);
-                        mj = kb + 4u * fl + ((uint32_t)__builtin_ctz(xf) >> 3);
-                        break;
-                    }
-                    kb += 4u * CW_LANES;
-                }
-                if (mj > limj) mj = limj;
-                if (lane == j) m = mj;
+                const uint32_t mj = cw_coop_len(L, P + last, readlane_u32(ref, last),
+                                                readlane_u32(m, last), readlane_u32(lim, last));
+                if (lane == last) m = mj;
+                NXc &= ~(1ull << last);
+                if (last + mj < lim_lane) { s0 = last + mj; continue; }
             }
-            if (j + mj >= lim_lane) {
-                exitLane = (int)j;
-                mexit = mj;
-                end = j + 1u;
-                break;
+            if ((MMc >> last) & 1ull) {
+                exitLane = (int)last;
+                mexit = readlane_u32(m, last);
+                end = last + 1u;
+            } else {
+                end = lim_lane;
             }
-            i0 = j + mj;
-        }
-        CW_PHASE(6);
-
-        /* 5. speculation check: prevW must be an inserted position */
-        const uint64_t INTR = ~V & ~(V >> 1) & ~(V >> 2);    /* inside a match */
-        const bool visited = (V >> lane) & 1ull;
-        const bool bad = visited && prevW >= 0 && ((INTR >> (uint32_t)prevW) & 1ull);
-        const uint64_t BAD = __ballot(bad);
-        uint32_t acc_end = end;            /* lanes [0, acc_end) are accepted */
-        bool byMatch = exitLane >= 0;
-        if (BAD) {
+            /* speculation check: prevW must be an inserted position */
+            const uint64_t INTR = ~V & ~(V >> 1) & ~(V >> 2);    /* inside a match */
+            const bool vis = (V >> lane) & 1ull;
+            const uint64_t BADC = __ballot(vis && prevW >= 0 && ((INTR >> (uint32_t)prevW) & 1ull));
+            if (!BADC) break;
+            /* lane f read an entry the reference never inserted: its ref is
+             * the latest INSERTED same-slot lane, else the table entry T */
             CW_STAT_ADD(trunc, 1);
-            acc_end = (uint32_t)__builtin_ctzll(BAD);
-            byMatch = false;
+            const uint32_t f = (uint32_t)__builtin_ctzll(BADC);
+            const uint64_t alt = readlane_u64(Ms, f) & lanemask_lt(f) & ~INTR;
+            const uint32_t rf = alt ? P + 63u - (uint32_t)__builtin_clzll(alt) : readlane_u32(T, f);
+            const uint32_t pf = P + f;
+            bool ok = rf != 0xFFFFFFFFu && rf > 0u && (pf - rf - 1u) < LZF_WINDOW && pf + 4u < n;
+            if (ok) ok = readlane_u32(L.rd4(rf) & 0xFFFFFFu, 0) == readlane_u32(tri, f);
+            const uint64_t fb = 1ull << f;
+            if (ok) {
+                const uint32_t mf = cw_coop_len(L, pf, rf, 3u, match_lim(n, pf));
+                MMc |= fb;
+                if (lane == f) { m = mf; ref = rf; }
+            } else {
+                MMc &= ~fb;
+            }
+            NXc &= ~fb;
+            if (lane == f) prevW = -1;
+            s0 = f;
+            exitLane = -1;
         }
-        const uint64_t ACC = lanemask_lt(acc_end);
-        CW_STAT_ADD(orbitm, (unsigned long long)__builtin_popcountll(MMV & ACC));
-        CW_PHASE(7);
+        const uint64_t MMV = MMc & V;
+        const uint64_t ACC = lanemask_lt(end);
+        const bool byMatch = exitLane >= 0;
+        CW_STAT_ADD(orbitm, (unsigned long long)__builtin_popcountll(MMV));
+        CW_PHASE(5);
 
-        /* 6. emission.  A segment = the visited lanes after one match up to
-         * and including the next; its literals are consecutive lanes. */
+        /* ---- 5. emission.  A segment = the visited lanes after one match
+         * up to and including the next; its literals are consecutive. ---- */
+        const bool visited = (V >> lane) & 1ull;
         const bool isM = (MMV >> lane) & 1ull;
         const uint64_t NVb = ~V & lanemask_lt(lane);
         const uint32_t segStart = NVb ? 64u - (uint32_t)__builtin_clzll(NVb) : 0u;
@@ -379,7 +474,7 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
         const uint32_t incl = wave_incl_sum(delta);
         const uint32_t myH0 = H0 + incl - delta;
         bool lfail = false;
-        if (visited && ((ACC >> lane) & 1ull)) {
+        if (visited) {
             if (!isM) {
                 const uint32_t pos = myH0 + nf;
                 if (pos >= cap) {
@@ -389,34 +484,34 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
                     if ((R & 31u) == 31u) dst[pos - 32u] = 31u;     /* rollover header */
                 }
             } else {
-                const uint32_t T = myH0 + Tr;
-                if (T + 4u >= cap) {
+                const uint32_t Tp = myH0 + Tr;
+                if (Tp + 4u >= cap) {
                     lfail = true;                                   /* src/lzf_c.c:176 */
                 } else {
                     if (R & 31u) dst[myH0 + 33u * (R >> 5)] = (uint8_t)((R & 31u) - 1u);
                     const uint32_t off = p - ref - 1u;
                     const uint32_t Lc = m - 2u;
                     if (Lc < 7u) {
-                        dst[T] = (uint8_t)((off >> 8) | (Lc << 5));
-                        dst[T + 1u] = (uint8_t)off;
+                        dst[Tp] = (uint8_t)((off >> 8) | (Lc << 5));
+                        dst[Tp + 1u] = (uint8_t)off;
                     } else {
-                        dst[T] = (uint8_t)((off >> 8) | 0xE0u);
-                        dst[T + 1u] = (uint8_t)(Lc - 7u);
-                        dst[T + 2u] = (uint8_t)off;
+                        dst[Tp] = (uint8_t)((off >> 8) | 0xE0u);
+                        dst[Tp + 1u] = (uint8_t)(Lc - 7u);
+                        dst[Tp + 2u] = (uint8_t)off;
                     }
                 }
             }
         }
         if (__ballot(lfail)) { fail = true; break; }
-        CW_PHASE(8);
+        CW_PHASE(6);
 
-        /* carry the cursor state to the next window */
+        /* ---- carry the cursor state to the next window ---------------- */
         uint32_t Pn;
         uint64_t INS = (V | (~V & ((V >> 1) | (V >> 2)))) & ACC;   /* visited + match tails */
         uint32_t tx0 = 0xFFFFFFFFu, tx1 = 0xFFFFFFFFu;           /* tails beyond the window */
         if (byMatch) {
             const uint32_t j = (uint32_t)exitLane;
-            H0 = H0 + __builtin_amdgcn_readlane(incl, j);
+            H0 = H0 + readlane_u32(incl, j);
             c0 = 0u;
             Pn = P + j + mexit;
             if (Pn + 2u < n) {                 /* src/lzf_c.c:229-247 */
@@ -425,38 +520,29 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
                 if (c < CW_LANES) INS |= 1ull << c; else tx1 = P + c;
             }
         } else {
-            const uint32_t e = acc_end;        /* first lane of the next window */
+            const uint32_t e = end;            /* == lim_lane: first lane of the next window */
             const uint64_t nvb = ~V & lanemask_lt(e);
             const uint32_t ss = nvb ? 64u - (uint32_t)__builtin_clzll(nvb) : 0u;
-            const uint32_t Re = ((MMV & lanemask_lt(e)) ? 0u : c0) + e - ss;
-            H0 = H0 + __builtin_amdgcn_readlane(incl, e - 1u) + 33u * (Re >> 5);
+            const uint32_t Re = (MMV ? 0u : c0) + e - ss;
+            H0 = H0 + readlane_u32(incl, e - 1u) + 33u * (Re >> 5);
             c0 = Re & 31u;
             Pn = P + e;
         }
 
-        /* 7. insert the window's inserted positions, in position order */
+        /* ---- 6. insert the window's inserted positions --------------- */
         if ((INS >> lane) & 1ull) {
-            const uint64_t same = M & INS & ~(1ull << lane);
-            const uint32_t myb = b << 16;
-            bool last = true;
-            int y = -1;        /* nearest earlier inserted lane, same bucket, other slot */
-            for (uint64_t c = same; c; c &= c - 1ull) {
-                const uint32_t j = (uint32_t)__builtin_ctzll(c);
-                const uint32_t e = L.sb[j];
-                if ((e & 0xFFFF0000u) != myb) continue;
-                if (j > lane) last = false;
-                else if ((e & 0xFFFFu) != s) y = (int)j;
+            const bool last = (Mb & INS & ~lanemask_lt(lane + 1u)) == 0ull;
+            const uint64_t other = Mb & ~Ms & INS & lanemask_lt(lane);
+            uint32_t y = 0xFFFFFFFFu;
+            if (other) {
+                y = P + 63u - (uint32_t)__builtin_clzll(other);
+            } else if (hv != H::NONE && p - H::pos(hv) <= LZF_WINDOW) {
+                const uint32_t hp = H::pos(hv);
+                if (H::slot(hv) != s) y = hp;
+                else if (L.chain[hp & L.cmask]) y = hp - L.chain[hp & L.cmask];
             }
-            uint32_t yp = 0xFFFFFFFFu;
-            if (y >= 0) {
-                yp = P + (uint32_t)y;
-            } else if (head_old != (uint32_t)NONE && p - head_old <= LZF_WINDOW) {
-                const uint32_t eh = L.chain[head_old & L.cmask];
-                if ((eh >> 16) != s) yp = head_old;
-                else if (eh & 0xFFFFu) yp = head_old - (eh & 0xFFFFu);
-            }
-            L.chain[p & L.cmask] = (s << 16) | ((yp != 0xFFFFFFFFu && p - yp <= LZF_WINDOW) ? p - yp : 0u);
-            if (last) L.head[b] = (HeadT)p;
+            L.chain[p & L.cmask] = (uint16_t)((y != 0xFFFFFFFFu && p - y <= LZF_WINDOW) ? p - y : 0u);
+            if (last) L.head[b] = H::make(s, p);
         }
         wave_lds_fence();
         if (tx0 != 0xFFFFFFFFu || tx1 != 0xFFFFFFFFu) {
@@ -466,7 +552,7 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
             }
             wave_lds_fence();
         }
-        CW_PHASE(9);
+        CW_PHASE(7);
         P = Pn;
     }
 #ifdef LZF_CW_STATS
@@ -514,8 +600,8 @@ static hipError_t launch_window(const LzfBatch &b, hipStream_t s)
 {
     const uint32_t ring = ring_for(b.max_len);
     const uint32_t chain = ring < CW_CHAIN ? ring : CW_CHAIN;
-    const size_t lds = ring + CW_KEYS * 8u + CW_LANES * 4u + CW_HBUCKETS * sizeof(HeadT) +
-                       chain * sizeof(uint32_t);
+    const size_t lds = ring + CW_HBUCKETS * sizeof(HeadT) + (64u + 64u + 16u) * 8u + CW_LANES * 4u +
+                       chain * sizeof(uint16_t);
     hipError_t e = hipFuncSetAttribute((const void *)lzf_compress_window_kernel<HeadT>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -526,8 +612,8 @@ static hipError_t launch_window(const LzfBatch &b, hipStream_t s)
 
 hipError_t lzf_launch_compress(const LzfBatch &b, hipStream_t s)
 {
-    if (b.max_len <= 65536u) return launch_window<uint16_t>(b, s);
-    return launch_window<uint32_t>(b, s);
+    if (b.max_len <= 65536u) return launch_window<uint32_t>(b, s);
+    return launch_window<unsigned long long>(b, s);
 }
 
 const char *lzf_compress_kernel_name(void) { return "window64"; }

@@ -10,8 +10,8 @@ import torch  # noqa: E402
 
 import gibson_amd  # noqa: E402
 
-PHASES = ["setup", "refill", "slots+keymask", "prevW", "lookup", "match+ext", "orbit",
-          "validate", "emit", "insert"]
+PHASES = ["setup", "refill", "slots+masks", "lookup", "match+probe", "orbit+repair",
+          "emit", "insert"]
 
 
 def main():
@@ -42,7 +42,7 @@ def main():
     w = max(1, st[0])
     print(f"kind {kind} n {n} count {count}: {e0.elapsed_time(e1):.2f} ms, "
           f"{count * n / e0.elapsed_time(e1) / 1e6:.2f} GB/s, ratio {float(ol.sum()) / (count * n):.4f}")
-    print(f"windows/value {st[0] / vals:.1f}  trunc/value {st[1] / vals:.2f}  "
+    print(f"windows/value {st[0] / vals:.1f}  repairs/value {st[1] / vals:.2f}  "
           f"hops/window {st[2] / w:.1f}  ext-iters/window {st[3] / w:.1f}  "
           f"orbit-matches/window {st[4] / w:.2f}  coop/window {st[6] / w:.2f}")
     tot = sum(st[8:8 + len(PHASES)])
