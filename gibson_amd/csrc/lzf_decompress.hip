@@ -1,4 +1,237 @@
-// decompress parallel generation: placeholder (serial kernel serves) until it lands
+/*
+ * lzf_decompress.hip -- token-parallel LZF decoder for gfx950.
+ *
+ * Replaces src/lzf_d.c:55-149 for batches of independent streams: one
+ * workgroup = one 64-lane wave per stream.  The stream is consumed in
+ * rounds; a round starts at a token boundary and covers the tokens that
+ * START in the next 64 input bytes:
+ *
+ *   1. token boundaries: every lane takes one input byte c and its token
+ *      size (literal c<32: c+2 bytes; back-ref: 2, or 3 when c>>5 == 7);
+ *      the chain of boundaries from lane 0 is found by pointer doubling
+ *      (ds_bpermute), as in the compressor's parse orbit;
+ *   2. each boundary lane decodes its token (src/lzf_d.c:66-119) and the
+ *      output offsets follow from one wave prefix sum (DPP) of the token
+ *      output lengths;
+ *   3. the reference's error checks, in its order (literal: E2BIG then
+ *      EINVAL, src/lzf_d.c:72-84; back-ref: EINVAL on a truncated token,
+ *      E2BIG, EINVAL on a reference before the output start,
+ *      src/lzf_d.c:100-131) -- the first failing token decides errno;
+ *   4. the output bytes are produced 64 at a time, one per lane: the owning
+ *      token comes from a max-scan of token-start marks, the byte from the
+ *      LDS input ring (literal) or the LDS output window (back-ref); a
+ *      back-ref byte whose source lies in the same 64-byte group (runs,
+ *      src/lzf_d.c:137-142 copies byte-serially so overlap replicates) is
+ *      resolved by pointer doubling over the group's lanes.  Every group is
+ *      stored to HBM as it completes.
+ */
 #include "lzf_internal.h"
-hipError_t lzf_launch_decompress(const LzfBatch &, hipStream_t) { return hipErrorNotSupported; }
-const char *lzf_decompress_kernel_name(void) { return nullptr; }
+
+#define CD_LANES   64u
+#define CD_IN_RING 4096u
+#define CD_OUT_MAX 16384u
+
+__device__ __forceinline__ uint64_t cd_lt(uint32_t i)
+{
+    return i >= 64u ? ~0ull : ((1ull << i) - 1ull);
+}
+
+__device__ __forceinline__ void cd_fence()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint32_t cd_incl_sum(uint32_t x)
+{
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
+}
+
+__device__ __forceinline__ uint32_t cd_incl_max(uint32_t x)
+{
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
+    return x;
+}
+
+__device__ __forceinline__ uint32_t cd_rl(uint32_t v, uint32_t l)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+
+__global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, uint32_t out_ring)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t *inr = smem;                               /* CD_IN_RING */
+    uint8_t *outr = smem + CD_IN_RING;                 /* out_ring (power of two) */
+    uint32_t *mark = (uint32_t *)(outr + out_ring);    /* 64 token-start marks */
+    uint32_t *flag = mark + CD_LANES;                  /* 64 orbit flags */
+    const uint32_t imask = CD_IN_RING - 1u, omask = out_ring - 1u;
+
+    const uint32_t lane = threadIdx.x;
+    const uint32_t v = blockIdx.x;
+    const uint32_t in_len = bt.in_len[v];
+    const uint32_t cap = bt.out_cap[v];
+    const uint8_t *src = bt.in + bt.in_off[v];
+    uint8_t *dst = bt.out + bt.out_off[v];
+    /* as the reference, a 0-length stream still reads its first control byte */
+    const uint32_t avail = in_len ? in_len : 1u;
+
+    uint32_t loaded = 0;
+    uint32_t base = 0;          /* input offset of the round's first token */
+    uint32_t O = 0;             /* output bytes produced so far */
+    int32_t err = 0;
+    bool first = true;
+
+    while (first || base < in_len) {                     /* src/lzf_d.c:64, 146 */
+        first = false;
+        /* stage input [base, base + 128) (tokens starting in the round and
+         * their literal payloads, <= 63 + 33 bytes) */
+        uint32_t need = base + 2u * CD_LANES;
+        if (need > avail) need = avail;
+        if (loaded < need) {
+            uint32_t to = loaded + 2048u;
+            if (to < need) to = need;
+            if (to > avail) to = avail;
+            for (uint32_t x = loaded + lane; x < to; x += CD_LANES) inr[x & imask] = src[x];
+            loaded = to;
+            cd_fence();
+        }
+
+        /* ---- 1. token boundaries -------------------------------------- */
+        const uint32_t ip = base + lane;
+        const uint32_t c = inr[ip & imask];
+        const uint32_t b1 = inr[(ip + 1u) & imask], b2 = inr[(ip + 2u) & imask];
+        const uint32_t tsz = c < 32u ? c + 2u : ((c >> 5) == 7u ? 3u : 2u);
+        uint32_t nx = lane + tsz;
+        if (ip + tsz >= in_len || nx > CD_LANES) nx = CD_LANES;   /* loop ends / next round */
+        uint32_t J0 = nx, J1, J2, J3, J4, J5;
+        J1 = J0 >= CD_LANES ? CD_LANES : (uint32_t)__shfl((int)J0, (int)J0);
+        J2 = J1 >= CD_LANES ? CD_LANES : (uint32_t)__shfl((int)J1, (int)J1);
+        J3 = J2 >= CD_LANES ? CD_LANES : (uint32_t)__shfl((int)J2, (int)J2);
+        J4 = J3 >= CD_LANES ? CD_LANES : (uint32_t)__shfl((int)J3, (int)J3);
+        J5 = J4 >= CD_LANES ? CD_LANES : (uint32_t)__shfl((int)J4, (int)J4);
+        uint32_t x = 0, y;
+        y = (uint32_t)__shfl((int)J0, (int)(x & 63u)); if ((lane & 1u) && x < CD_LANES) x = y;
+        y = (uint32_t)__shfl((int)J1, (int)(x & 63u)); if ((lane & 2u) && x < CD_LANES) x = y;
+        y = (uint32_t)__shfl((int)J2, (int)(x & 63u)); if ((lane & 4u) && x < CD_LANES) x = y;
+        y = (uint32_t)__shfl((int)J3, (int)(x & 63u)); if ((lane & 8u) && x < CD_LANES) x = y;
+        y = (uint32_t)__shfl((int)J4, (int)(x & 63u)); if ((lane & 16u) && x < CD_LANES) x = y;
+        y = (uint32_t)__shfl((int)J5, (int)(x & 63u)); if ((lane & 32u) && x < CD_LANES) x = y;
+        flag[lane] = 0u;
+        cd_fence();
+        if (x < CD_LANES) flag[x] = 1u;
+        cd_fence();
+        const uint64_t TS = __ballot(flag[lane] != 0u);
+        const uint32_t lastT = 63u - (uint32_t)__builtin_clzll(TS);
+        const bool tok = (TS >> lane) & 1ull;
+
+        /* ---- 2. decode + output offsets ------------------------------- */
+        const bool lit = c < 32u;
+        uint32_t olen, back = 0, lsrc = 0;
+        int32_t e = 0;
+        if (lit) {
+            olen = c + 1u;
+            lsrc = ip + 1u;
+        } else {
+            uint32_t len = c >> 5, offb = b1;
+            if (len == 7u) { len += b1; offb = b2; }
+            olen = len + 2u;
+            back = ((c & 31u) << 8) + offb + 1u;
+        }
+        const uint32_t tinfo = lit ? lsrc : back;          /* literal source / distance */
+        const uint32_t ol = tok ? olen : 0u;
+        const uint32_t incl = cd_incl_sum(ol);
+        const uint32_t Ot = O + incl - ol;                 /* output offset of my token */
+        /* ---- 3. the reference's checks, in its order ------------------ */
+        if (tok) {
+            if (lit) {
+                if ((uint64_t)Ot + olen > cap) e = 7;                       /* E2BIG  :72 */
+                else if ((uint64_t)ip + 1u + olen > in_len) e = 22;         /* EINVAL :79 */
+            } else {
+                if (ip + 1u >= in_len) e = 22;                              /* :101 */
+                else if ((c >> 5) == 7u && ip + 2u >= in_len) e = 22;      /* :111 */
+                else if ((uint64_t)Ot + olen > cap) e = 7;                  /* :121 */
+                else if (back > Ot) e = 22;                                 /* :127 */
+            }
+        }
+        const uint64_t EB = __ballot(e != 0);
+        if (EB) {
+            err = (int32_t)cd_rl((uint32_t)e, (uint32_t)__builtin_ctzll(EB));
+            break;
+        }
+        const uint32_t total = cd_rl(incl, 63u);           /* round output bytes */
+
+        /* ---- 4. output bytes, 64 per step ------------------------------ */
+        uint32_t carry = 0;          /* token lane owning the first byte of the group */
+        for (uint32_t g = 0; g < total; g += CD_LANES) {
+            const uint32_t gb = O + g;                     /* group's first output offset */
+            mark[lane] = 0u;
+            cd_fence();
+            if (tok && Ot >= gb && Ot < gb + CD_LANES) mark[Ot - gb] = lane + 1u;
+            cd_fence();
+            uint32_t k = cd_incl_max(mark[lane]);
+            k = k ? k - 1u : carry;
+            carry = cd_rl(k, 63u);
+            const uint32_t o = gb + lane;
+            const bool live = g + lane < total;
+            const uint32_t tO = (uint32_t)__shfl((int)Ot, (int)k);
+            const uint32_t tLit = (uint32_t)__shfl((int)lit, (int)k);
+            const uint32_t tSrc = (uint32_t)__shfl((int)tinfo, (int)k);
+            uint32_t val = 0;
+            int ptr = -1;
+            if (live) {
+                if (tLit) {
+                    val = inr[(tSrc + (o - tO)) & imask];
+                } else {
+                    const uint32_t so = o - tSrc;
+                    if (so >= gb) ptr = (int)(so - gb);
+                    else val = outr[so & omask];
+                }
+            }
+            /* in-group back-references (runs): pointer doubling */
+            while (__ballot(ptr >= 0)) {
+                const int pi = ptr >= 0 ? ptr : (int)lane;
+                const uint32_t pv = (uint32_t)__shfl((int)val, pi);
+                const int pp = __shfl(ptr, pi);
+                if (ptr >= 0) { val = pv; ptr = pp; }
+            }
+            if (live) {
+                outr[o & omask] = (uint8_t)val;
+                dst[o] = (uint8_t)val;
+            }
+            cd_fence();
+        }
+        O += total;
+        /* next round: the token after the last one of this round */
+        base = base + cd_rl(nx == CD_LANES ? lane + tsz : nx, lastT);
+    }
+    if (lane == 0) {
+        bt.out_len[v] = err ? 0u : O;
+        bt.err[v] = err;
+    }
+}
+
+hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s)
+{
+    uint32_t ring = 256u;
+    while (ring < b.max_len && ring < CD_OUT_MAX) ring <<= 1;
+    const size_t lds = CD_IN_RING + ring + 2u * CD_LANES * 4u;
+    hipError_t e = hipFuncSetAttribute((const void *)lzf_decompress_tokpar_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(lzf_decompress_tokpar_kernel, dim3(b.count), dim3(CD_LANES), lds, s, b, ring);
+    return hipGetLastError();
+}
+
+const char *lzf_decompress_kernel_name(void) { return "tokpar64"; }
