@@ -89,6 +89,18 @@ def cpu_baseline(kind, seed, n, count, threads):
     }
 
 
+def _traffic(workload, kernel, count):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (profiles/traffic_<workload>.json, tools/traffic.py: 2*FETCH_SIZE +
+    WRITE_SIZE, KiB -> B, gfx950 read-side correction), or None."""
+    f = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
+    try:
+        t = json.load(open(f))
+        return int(t["kernels"][kernel]["bytes_per_value"] * count)
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -226,14 +238,15 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBPS, 5),
-                "traffic": None,
+                "traffic": _traffic(a.workload, dom, count),
+                "algorithmic_bytes": kern[dom][0],
                 "per_kernel_ms": {k: round(v[1] * 1e3, 3) for k, v in kern.items()},
                 "per_kernel_GBps": {k: round(v[0] / v[1] / 1e9, 2) for k, v in kern.items()},
             },
         }
         if world == 1 and not a.no_cpu:
             threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-            cnt = a.cpu_count or max(64, (256 << 20) // n)
+            cnt = a.cpu_count or min(count, max(64, (4 << 30) // n))
             line["cpu_baseline"] = cpu_baseline(kind, seed, n, cnt, threads)
         print(json.dumps(line), flush=True)
     if world > 1:
