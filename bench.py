@@ -33,6 +33,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 import gibson_amd  # noqa: E402
+from gibson_amd.shard import reduce_stats, shard  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -128,7 +129,8 @@ def main():
 
     # ---- data in HBM: value i of this rank is global value rank + k*world ----
     src = torch.empty(count * n, dtype=torch.uint8, device=dev)
-    gibson_amd.synth_fill(kind, seed, rank, world, count, n, src)
+    first, stride = shard(rank, world)
+    gibson_amd.synth_fill(kind, seed, first, stride, count, n, src)
     off = torch.arange(count, dtype=torch.int64, device=dev) * n
     in_len = torch.full((count,), n, dtype=torch.int32, device=dev)
     ccap = torch.full((count,), n - 4, dtype=torch.int32, device=dev)
@@ -185,14 +187,8 @@ def main():
         diff = (dv[r0:r1] != sv[r0:r1]).any(dim=1) & ok[r0:r1]
         good = good and not bool(diff.any())
 
-    stats = torch.tensor([wall, t_comp, t_dec], dtype=torch.float64, device=dev)
-    tot = torch.tensor([count * n, n_ok, c_bytes, 0 if good else 1], dtype=torch.float64,
-                       device=dev)
-    if world > 1:
-        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    wall, t_comp, t_dec = stats.tolist()
-    in_bytes_all, n_ok_all, c_bytes_all, bad_ranks = tot.tolist()
+    (wall, t_comp, t_dec), (in_bytes_all, n_ok_all, c_bytes_all, bad_ranks) = reduce_stats(
+        [wall, t_comp, t_dec], [count * n, n_ok, c_bytes, 0 if good else 1], device=dev)
 
     if rank == 0:
         sec_per_step = wall / a.steps
