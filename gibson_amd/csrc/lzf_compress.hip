@@ -215,6 +215,62 @@ __device__ __forceinline__ uint32_t cw_coop_len(const CwLds<HeadT> &L, uint32_t 
     return lim;
 }
 
+/* Latest inserted position < P with slot s (or none), from the bucket head
+ * hv and the skip chain; exactly the reference's table entry when it is
+ * within the 8 KiB window (src/lzf_c.c:147-155). */
+template <typename HeadT>
+__device__ __forceinline__ uint32_t cw_lookup(const CwLds<HeadT> &L, HeadT hv, uint32_t s, uint32_t p)
+{
+    typedef HeadOps<HeadT> H;
+    if (hv == H::NONE) return 0xFFFFFFFFu;
+    uint32_t q = H::pos(hv), sq = H::slot(hv);
+    while (p - q <= LZF_WINDOW) {
+        if (sq == s) return q;
+        const uint32_t d = L.chain[q & L.cmask];      /* skip q's run of its slot */
+        if (d == 0u) break;
+        q -= d;
+        sq = slot_of(L.rd4(q) & 0xFFFFFFu);
+    }
+    return 0xFFFFFFFFu;
+}
+
+/* First mismatch index in [3, kc) of p vs r (kc <= 19), or kc: five aligned
+ * dwords per side, no loop. */
+template <typename HeadT>
+__device__ __forceinline__ uint32_t cw_probe(const CwLds<HeadT> &L, uint32_t p, uint32_t r, uint32_t kc)
+{
+    const uint32_t *w = (const uint32_t *)L.ring;
+    const uint32_t wm = L.rmask >> 2;
+    const uint32_t pa = (p + 3u) >> 2, ra = (r + 3u) >> 2;
+    const uint32_t ps = (p + 3u) & 3u, rs = (r + 3u) & 3u;
+    uint32_t pw[5], rw[5];
+#pragma unroll
+    for (int t = 0; t < 5; t++) {
+        pw[t] = w[(pa + t) & wm];
+        rw[t] = w[(ra + t) & wm];
+    }
+    uint32_t k = kc;
+#pragma unroll
+    for (int t = 3; t >= 0; t--) {
+        const uint32_t x = __builtin_amdgcn_alignbyte(pw[t + 1], pw[t], ps) ^
+                           __builtin_amdgcn_alignbyte(rw[t + 1], rw[t], rs);
+        if (x) k = 3u + 4u * (uint32_t)t + ((uint32_t)__builtin_ctz(x) >> 3);
+    }
+    return k < kc ? k : kc;
+}
+
+/* Inclusive max over the 64 lanes (DPP). */
+__device__ __forceinline__ uint32_t cd_incl_max(uint32_t x)
+{
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
+    return x;
+}
+
 __device__ __forceinline__ uint32_t match_lim(uint32_t n, uint32_t p)
 {
     uint32_t maxlen = n - p - 2u;
@@ -334,19 +390,9 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
         int prevW = msb ? (int)(63u - (uint32_t)__builtin_clzll(msb)) : -1;
         CW_PHASE(2);
 
-        /* ---- 2. exact table lookup among positions < P (all lanes) ---- */
+        /* ---- 2. exact table lookup among positions < P --------------- */
         uint32_t T = 0xFFFFFFFFu;
-        if (valid && hv != H::NONE) {
-            uint32_t q = H::pos(hv), sq = H::slot(hv);
-            while (p - q <= LZF_WINDOW) {
-                if (sq == s) { T = q; break; }
-                CW_STAT_ADD(hops, 1);
-                const uint32_t d = L.chain[q & L.cmask];   /* skip q's run of its slot */
-                if (d == 0u) break;
-                q -= d;
-                sq = slot_of(L.rd4(q) & 0xFFFFFFu);
-            }
-        }
+        if (valid && prevW < 0) T = cw_lookup<HeadT>(L, hv, s, p);
         CW_PHASE(3);
 
         /* ---- 3. match test (src/lzf_c.c:151-166), probed length ------ */
@@ -359,85 +405,80 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
         if (match) {
             lim = match_lim(n, p);
             const uint32_t kc = lim < CW_EXT_CAP ? lim : CW_EXT_CAP;
-            uint32_t k = 3u;
-            while (k < kc) {
-                CW_STAT_ADD(ext, 1);
-                uint32_t x = L.rd4(p + k) ^ L.rd4(ref + k);
-                const uint32_t rem = kc - k;
-                if (rem < 4u) x |= 0xFFFFFFFFu << (8u * rem);
-                if (x) { k += (uint32_t)__builtin_ctz(x) >> 3; break; }
-                k += 4u;
-            }
-            m = k < kc ? k : kc;
+            m = cw_probe(L, p, ref, kc);        /* bytes [3, kc) in one go */
             exact = (m < kc) || (kc == lim);
         }
         CW_PHASE(4);
 
         /* ---- 4. the parse orbit -----------------------------------------
-         * Pointer doubling: nxt(i) = i+1 (literal) or i+m (match), J_k =
-         * nxt^(2^k); lane t computes J^t(s0) and flags that lane, so one
-         * pass yields every visited lane from s0 on.  A pass stops at a match
-         * whose length is still only a lower bound (resolved by a whole-wave
-         * compare) and is redone from a lane whose speculative ref was not
-         * inserted (repaired in place, see step 4 in the header). */
+         * Literal lanes advance by one, so the orbit is fixed by the match
+         * lanes on it: nm(i) = first match lane >= i+m (i+1 for a
+         * literal), precomputed by every lane; a scalar walk follows nm
+         * through the match lanes only (v_readlane), a long match on it
+         * gets its exact length by a whole-wave compare, and the visited
+         * lanes follow from one prefix max of the matches' reach.  A lane
+         * whose prevW turns out to lie inside a match (never inserted by the
+         * reference) is repaired in place and the walk resumes there. */
         uint64_t MMc = __ballot(match) & lanemask_lt(lim_lane);
         uint64_t NXc = __ballot(!exact) & MMc;
-        uint64_t V = 0;
-        uint32_t s0 = 0, end = lim_lane, mexit = 0;
+        uint64_t MMV = 0, V = 0;
+        uint32_t end = lim_lane, mexit = 0, j0 = 0;
         int exitLane = -1;
         for (;;) {
-            /* one doubling pass from s0 */
-            const bool mine_m = (MMc >> lane) & 1ull;
-            uint32_t nx = lane + (mine_m ? m : 1u);
-            if (lane >= lim_lane || nx > CW_LANES || ((NXc >> lane) & 1ull)) nx = CW_LANES;
-            uint32_t J0 = nx, J1, J2, J3, J4, J5;
-            J1 = J0 >= CW_LANES ? CW_LANES : (uint32_t)__shfl((int)J0, (int)J0);
-            J2 = J1 >= CW_LANES ? CW_LANES : (uint32_t)__shfl((int)J1, (int)J1);
-            J3 = J2 >= CW_LANES ? CW_LANES : (uint32_t)__shfl((int)J2, (int)J2);
-            J4 = J3 >= CW_LANES ? CW_LANES : (uint32_t)__shfl((int)J3, (int)J3);
-            J5 = J4 >= CW_LANES ? CW_LANES : (uint32_t)__shfl((int)J4, (int)J4);
-            uint32_t x = s0, y;
-            y = (uint32_t)__shfl((int)J0, (int)(x & 63u)); if ((lane & 1u) && x < CW_LANES) x = y;
-            y = (uint32_t)__shfl((int)J1, (int)(x & 63u)); if ((lane & 2u) && x < CW_LANES) x = y;
-            y = (uint32_t)__shfl((int)J2, (int)(x & 63u)); if ((lane & 4u) && x < CW_LANES) x = y;
-            y = (uint32_t)__shfl((int)J3, (int)(x & 63u)); if ((lane & 8u) && x < CW_LANES) x = y;
-            y = (uint32_t)__shfl((int)J4, (int)(x & 63u)); if ((lane & 16u) && x < CW_LANES) x = y;
-            y = (uint32_t)__shfl((int)J5, (int)(x & 63u)); if ((lane & 32u) && x < CW_LANES) x = y;
-            L.flag[lane] = 0u;
-            wave_lds_fence();
-            if (x < CW_LANES) L.flag[x] = 1u;
-            wave_lds_fence();
-            const uint64_t Vp = __ballot(L.flag[lane] != 0u) & lanemask_lt(lim_lane);
-            V = (V & lanemask_lt(s0)) | Vp;
-            const uint32_t last = 63u - (uint32_t)__builtin_clzll(V);
-            if ((NXc >> last) & 1ull) {
-                /* a long match on the orbit: exact length, 256 B per step */
-                CW_STAT_ADD(coop, 1);
-                const uint32_t mj = cw_coop_len(L, P + last, readlane_u32(ref, last),
-                                                readlane_u32(m, last), readlane_u32(lim, last));
-                if (lane == last) m = mj;
-                NXc &= ~(1ull << last);
-                if (last + mj < lim_lane) { s0 = last + mj; continue; }
+            /* per-lane successor on the orbit */
+            const bool isMatch = (MMc >> lane) & 1ull;
+            const uint32_t tgt = lane + (isMatch ? m : 1u);
+            const uint64_t after = tgt >= CW_LANES ? 0ull : (MMc & ~lanemask_lt(tgt));
+            uint32_t nm = after ? (uint32_t)__builtin_ctzll(after) : CW_LANES;
+            if (isMatch && tgt >= lim_lane) nm = 255u;                /* leaves the window */
+            /* walk the match lanes of the orbit from j0 */
+            const uint64_t first = MMc & ~lanemask_lt(j0);
+            uint32_t j = first ? (uint32_t)__builtin_ctzll(first) : CW_LANES;
+            exitLane = -1;
+            while (j < lim_lane) {
+                MMV |= 1ull << j;
+                if ((NXc >> j) & 1ull) {
+                    CW_STAT_ADD(coop, 1);
+                    const uint32_t mj = cw_coop_len(L, P + j, readlane_u32(ref, j),
+                                                    readlane_u32(m, j), readlane_u32(lim, j));
+                    if (lane == j) m = mj;
+                    NXc &= ~(1ull << j);
+                    if (j + mj >= lim_lane) { exitLane = (int)j; mexit = mj; break; }
+                    const uint64_t a = MMc & ~lanemask_lt(j + mj);
+                    j = a ? (uint32_t)__builtin_ctzll(a) : CW_LANES;
+                } else {
+                    const uint32_t nj = readlane_u32(nm, j);
+                    if (nj == 255u) { exitLane = (int)j; mexit = readlane_u32(m, j); break; }
+                    j = nj;
+                }
             }
-            if ((MMc >> last) & 1ull) {
-                exitLane = (int)last;
-                mexit = readlane_u32(m, last);
-                end = last + 1u;
-            } else {
-                end = lim_lane;
-            }
+            end = exitLane >= 0 ? (uint32_t)exitLane + 1u : lim_lane;
+            /* visited = not strictly inside the reach of an earlier orbit match */
+            const uint32_t reach = ((MMV >> lane) & 1ull) ? lane + m : 0u;
+            uint32_t before = (uint32_t)__shfl_up((int)reach, 1);
+            if (lane == 0) before = 0u;
+            const uint32_t rmax = cd_incl_max(before);
+            V = __ballot(rmax <= lane) & lanemask_lt(end);
             /* speculation check: prevW must be an inserted position */
             const uint64_t INTR = ~V & ~(V >> 1) & ~(V >> 2);    /* inside a match */
             const bool vis = (V >> lane) & 1ull;
             const uint64_t BADC = __ballot(vis && prevW >= 0 && ((INTR >> (uint32_t)prevW) & 1ull));
             if (!BADC) break;
             /* lane f read an entry the reference never inserted: its ref is
-             * the latest INSERTED same-slot lane, else the table entry T */
+             * the latest INSERTED same-slot lane, else the table entry */
             CW_STAT_ADD(trunc, 1);
             const uint32_t f = (uint32_t)__builtin_ctzll(BADC);
             const uint64_t alt = readlane_u64(Ms, f) & lanemask_lt(f) & ~INTR;
-            const uint32_t rf = alt ? P + 63u - (uint32_t)__builtin_clzll(alt) : readlane_u32(T, f);
             const uint32_t pf = P + f;
+            uint32_t rf;
+            if (alt) {
+                rf = P + 63u - (uint32_t)__builtin_clzll(alt);
+            } else {
+                HeadT hf;
+                if constexpr (sizeof(HeadT) == 8) hf = (HeadT)readlane_u64((uint64_t)hv, f);
+                else hf = (HeadT)readlane_u32((uint32_t)hv, f);
+                rf = cw_lookup<HeadT>(L, hf, readlane_u32(s, f), pf);
+            }
             bool ok = rf != 0xFFFFFFFFu && rf > 0u && (pf - rf - 1u) < LZF_WINDOW && pf + 4u < n;
             if (ok) ok = readlane_u32(L.rd4(rf) & 0xFFFFFFu, 0) == readlane_u32(tri, f);
             const uint64_t fb = 1ull << f;
@@ -450,10 +491,9 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
             }
             NXc &= ~fb;
             if (lane == f) prevW = -1;
-            s0 = f;
-            exitLane = -1;
+            MMV &= lanemask_lt(f);
+            j0 = f;
         }
-        const uint64_t MMV = MMc & V;
         const uint64_t ACC = lanemask_lt(end);
         const bool byMatch = exitLane >= 0;
         CW_STAT_ADD(orbitm, (unsigned long long)__builtin_popcountll(MMV));
