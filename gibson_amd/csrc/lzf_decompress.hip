@@ -174,7 +174,11 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
 
         /* ---- 4. output bytes, 64 per step ------------------------------ */
         uint32_t carry = 0;          /* token lane owning the first byte of the group */
+#ifdef LZF_CD_ABLATE_OUTPUT           /* diagnostic builds only: time discovery alone */
+        for (uint32_t g = 0; g < 0u; g += CD_LANES) {
+#else
         for (uint32_t g = 0; g < total; g += CD_LANES) {
+#endif
             const uint32_t gb = O + g;                     /* group's first output offset */
             mark[lane] = 0u;
             cd_fence();

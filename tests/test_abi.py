@@ -68,3 +68,20 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
         raise AssertionError("missing library must raise")
     finally:
         importlib.reload(m)
+
+
+def test_batch_calls_reject_bad_arguments_without_device():
+    # argument validation happens before any HIP call, so this runs on CPU
+    import ctypes
+    L = gibson_amd.lib()
+    null = ctypes.c_void_p(0)
+    buf = ctypes.create_string_buffer(64)
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    assert L.lzf_gpu_compress_batch(null, p, p, p, p, p, p, 1, 16, null) == -1
+    assert L.lzf_gpu_compress_batch(p, p, p, p, p, p, p, 0, 16, null) == -1
+    assert L.lzf_gpu_compress_batch(p, p, p, p, p, p, p, 1, (64 << 20) + 1, null) == -1
+    assert L.lzf_gpu_decompress_batch(p, p, p, p, p, p, p, null, 1, 16, null) == -1
+    assert L.lzf_gpu_decompress_batch(p, p, p, p, p, p, p, p, 0, 16, null) == -1
+    assert L.lzf_gpu_synth_fill(0, 0, 0, 1, 0, 16, p, null) == -1
+    assert L.lzf_host_compress_batch(null, p, p, p, p, p, p, 1) == -1
+    assert L.lzf_host_decompress_batch(p, p, p, p, p, p, p, null, 0) == -1

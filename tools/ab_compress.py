@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Interleaved A/B timing of the compress kernel across library builds (one
-process, same device; cdna_hip_programming.md §5.4 rule 24).
-usage: ab_compress.py KIND N COUNT ROUNDS LIB_A LIB_B [...]"""
+"""Interleaved A/B timing of the compress (or, with AB_MODE=decompress, the
+decompress) kernel across library builds: one process, same device
+(cdna_hip_programming.md §5.4 rule 24).
+usage: [AB_MODE=decompress] ab_compress.py KIND N COUNT ROUNDS LIB_A LIB_B [...]"""
 import ctypes
 import os
 import sys
@@ -14,6 +15,7 @@ def load(path):
     L = ctypes.CDLL(path)
     vp, u32 = ctypes.c_void_p, ctypes.c_uint32
     L.lzf_gpu_compress_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, u32, vp]
+    L.lzf_gpu_decompress_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, u32, vp]
     L.lzf_gpu_synth_fill.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                      u32, u32, vp, vp]
     return L
@@ -33,6 +35,36 @@ def main():
     outs = []
     res = {p: [] for p, _ in libs}
     P = lambda t: ctypes.c_void_p(t.data_ptr())
+    if os.environ.get("AB_MODE") == "decompress":
+        comp = torch.empty(count * n, dtype=torch.uint8, device=dev)
+        cl = torch.zeros(count, dtype=torch.int32, device=dev)
+        libs[0][1].lzf_gpu_compress_batch(P(src), P(off), P(ln), P(comp), P(off), P(cap), P(cl), count, n, h)
+        dcap = torch.full((count,), n, dtype=torch.int32, device=dev)
+        for r in range(rounds + 1):
+            for p, L in libs:
+                out = torch.zeros(count * n, dtype=torch.uint8, device=dev)
+                ol = torch.zeros(count, dtype=torch.int32, device=dev)
+                er = torch.zeros(count, dtype=torch.int32, device=dev)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                rc = L.lzf_gpu_decompress_batch(P(comp), P(off), P(cl), P(out), P(off), P(dcap), P(ol),
+                                                P(er), count, n, h)
+                e1.record(s)
+                torch.cuda.synchronize()
+                assert rc == 0
+                if r:
+                    res[p].append(e0.elapsed_time(e1))
+                if r == 1:
+                    ok = cl > 0
+                    good = bool(((ol == n) | ~ok).all()) and all(
+                        torch.equal(out.view(count, n)[i], src.view(count, n)[i])
+                        for i in range(0, count, max(1, count // 256)) if bool(ok[i]))
+                    print(f"{os.path.basename(p)} round trip ok: {good}")
+        for p, t in res.items():
+            t.sort()
+            print(f"{os.path.basename(p):28s} median {t[len(t) // 2]:8.2f} ms  min {t[0]:8.2f}  "
+                  f"{count * n / t[len(t) // 2] / 1e6:7.2f} GB/s (decompress, output bytes)")
+        return
     for r in range(rounds + 1):
         for p, L in libs:
             out = torch.empty(count * n, dtype=torch.uint8, device=dev)
