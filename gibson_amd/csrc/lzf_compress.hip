@@ -43,8 +43,16 @@
 #include "lzf_internal.h"
 
 #define CW_LANES     64u
+#ifndef CW_HBITS
 #define CW_HBITS     10
+#endif
 #define CW_HBUCKETS  (1u << CW_HBITS)
+/* lane bitmaps keyed by slot-mix bits [0,16-HBITS), [16-HBITS,12), [12,16):
+ * same slot = all three agree, same bucket = the last two agree */
+#define CW_T1        (1u << (16 - CW_HBITS))
+#define CW_T2        (1u << (CW_HBITS - 4))
+#define CW_T3        16u
+#define CW_TALL      (CW_T1 + CW_T2 + CW_T3)
 #define CW_CHAIN     8192u
 #define CW_RING_MAX  16384u
 #define CW_EXT_CAP   19u          /* per-lane match length probe (3 + 4 x 4 bytes) */
@@ -132,7 +140,6 @@ struct CwLds {
     uint32_t cmask;       /* chain ring entries - 1 */
     unsigned long long *t1, *t2, *t3;   /* window lane bitmaps keyed by slot-mix bits
                                          * 0-5, 6-11, 12-15 */
-    uint32_t *flag;       /* 64 orbit flags */
 
     __device__ __forceinline__ uint32_t rd4(uint32_t x) const
     {
@@ -298,10 +305,9 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
     L.rmask = ring_bytes - 1u;
     uint8_t *cur = smem + ring_bytes;
     L.head = (HeadT *)cur;                   cur += CW_HBUCKETS * sizeof(HeadT);
-    L.t1 = (unsigned long long *)cur;        cur += 64u * 8u;
-    L.t2 = (unsigned long long *)cur;        cur += 64u * 8u;
-    L.t3 = (unsigned long long *)cur;        cur += 16u * 8u;
-    L.flag = (uint32_t *)cur;                cur += CW_LANES * 4u;
+    L.t1 = (unsigned long long *)cur;        cur += CW_T1 * 8u;
+    L.t2 = (unsigned long long *)cur;        cur += CW_T2 * 8u;
+    L.t3 = (unsigned long long *)cur;        cur += CW_T3 * 8u;
     L.chain = (uint16_t *)cur;
     L.cmask = (ring_bytes < CW_CHAIN ? ring_bytes : CW_CHAIN) - 1u;
 
@@ -326,7 +332,7 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
         uint32_t *z = (uint32_t *)L.head;   /* heads = NONE, bitmaps = 0 */
         const uint32_t nh = CW_HBUCKETS * sizeof(HeadT) / 4u;
         for (uint32_t k = lane; k < nh; k += CW_LANES) z[k] = ~0u;
-        for (uint32_t k = lane; k < (64u + 64u + 16u) * 2u; k += CW_LANES) z[nh + k] = 0u;
+        for (uint32_t k = lane; k < CW_TALL * 2u; k += CW_LANES) z[nh + k] = 0u;
     }
     uint32_t loaded = n < ring_bytes ? n : ring_bytes;
     cw_fill(L, src, 0u, loaded);
@@ -362,7 +368,7 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
         const uint32_t s = slot_of(tri);
         const uint32_t sm = slot_mix(s);          /* bijective 16-bit mix of the slot */
         const uint32_t b = bucket_of(sm);
-        const uint32_t k1 = sm & 63u, k2 = (sm >> 6) & 63u, k3 = sm >> 12;
+        const uint32_t k1 = sm & (CW_T1 - 1u), k2 = (sm >> (16 - CW_HBITS)) & (CW_T2 - 1u), k3 = sm >> 12;
         const unsigned long long me = 1ull << lane;
         if (valid) {
             atomicOr(&L.t1[k1], me);
@@ -640,7 +646,7 @@ static hipError_t launch_window(const LzfBatch &b, hipStream_t s)
 {
     const uint32_t ring = ring_for(b.max_len);
     const uint32_t chain = ring < CW_CHAIN ? ring : CW_CHAIN;
-    const size_t lds = ring + CW_HBUCKETS * sizeof(HeadT) + (64u + 64u + 16u) * 8u + CW_LANES * 4u +
+    const size_t lds = ring + CW_HBUCKETS * sizeof(HeadT) + CW_TALL * 8u +
                        chain * sizeof(uint16_t);
     hipError_t e = hipFuncSetAttribute((const void *)lzf_compress_window_kernel<HeadT>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
