@@ -130,7 +130,7 @@ template <> struct HeadOps<unsigned long long> {
     __device__ static uint32_t slot(unsigned long long e) { return (uint32_t)(e >> 32); }
 };
 
-template <typename HeadT>
+template <typename HeadT, bool WRAP>
 struct CwLds {
     uint8_t *ring;        /* input ring, R bytes (power of two) */
     uint32_t rmask;       /* R - 1 */
@@ -141,19 +141,22 @@ struct CwLds {
     unsigned long long *t1, *t2, *t3;   /* window lane bitmaps keyed by slot-mix bits
                                          * 0-5, 6-11, 12-15 */
 
+    /* ring word / chain entry index: the ring and chain wrap only when the
+     * value is longer than them (WRAP); otherwise indices are positions */
+    __device__ __forceinline__ uint32_t wi(uint32_t w) const { return WRAP ? (w & (rmask >> 2)) : w; }
+    __device__ __forceinline__ uint32_t ci(uint32_t x) const { return WRAP ? (x & cmask) : x; }
     __device__ __forceinline__ uint32_t rd4(uint32_t x) const
     {
         const uint32_t *w = (const uint32_t *)ring;
-        uint32_t m = rmask >> 2;
-        uint32_t lo = w[(x >> 2) & m], hi = w[((x >> 2) + 1u) & m];
+        uint32_t lo = w[wi(x >> 2)], hi = w[wi((x >> 2) + 1u)];
         return __builtin_amdgcn_alignbyte(hi, lo, x & 3u);
     }
-    __device__ __forceinline__ uint32_t rd1(uint32_t x) const { return ring[x & rmask]; }
+    __device__ __forceinline__ uint32_t rd1(uint32_t x) const { return ring[WRAP ? (x & rmask) : x]; }
 };
 
 /* Stream input bytes [from, to) of the value into the ring. */
-template <typename HeadT>
-__device__ void cw_fill(const CwLds<HeadT> &L, const uint8_t *src, uint32_t from, uint32_t to)
+template <typename HeadT, bool WRAP>
+__device__ void cw_fill(const CwLds<HeadT, WRAP> &L, const uint8_t *src, uint32_t from, uint32_t to)
 {
     const uint32_t lane = threadIdx.x;
     if (((uintptr_t)(src + from) & 15u) == 0u) {
@@ -178,8 +181,8 @@ __device__ __forceinline__ uint32_t slot_mix(uint32_t s) { return (s * 40503u) &
 __device__ __forceinline__ uint32_t bucket_of(uint32_t sm) { return sm >> (16 - CW_HBITS); }
 
 /* Insert position x (slot sx) after every earlier position (one lane). */
-template <typename HeadT>
-__device__ __forceinline__ void cw_insert_one(const CwLds<HeadT> &L, uint32_t x, uint32_t sx)
+template <typename HeadT, bool WRAP>
+__device__ __forceinline__ void cw_insert_one(const CwLds<HeadT, WRAP> &L, uint32_t x, uint32_t sx)
 {
     typedef HeadOps<HeadT> H;
     const uint32_t bx = bucket_of(slot_mix(sx));
@@ -188,16 +191,16 @@ __device__ __forceinline__ void cw_insert_one(const CwLds<HeadT> &L, uint32_t x,
     if (hv != H::NONE && x - H::pos(hv) <= LZF_WINDOW) {
         const uint32_t hp = H::pos(hv);
         if (H::slot(hv) != sx) y = hp;
-        else if (L.chain[hp & L.cmask]) y = hp - L.chain[hp & L.cmask];
+        else if (L.chain[L.ci(hp)]) y = hp - L.chain[L.ci(hp)];
     }
-    L.chain[x & L.cmask] = (uint16_t)((y != 0xFFFFFFFFu && x - y <= LZF_WINDOW) ? x - y : 0u);
+    L.chain[L.ci(x)] = (uint16_t)((y != 0xFFFFFFFFu && x - y <= LZF_WINDOW) ? x - y : 0u);
     L.head[bx] = H::make(sx, x);
 }
 
 /* Length of the match p/r whose first k0 bytes are known equal, up to lim:
  * the whole wave compares 256 bytes per step (uniform inputs and result). */
-template <typename HeadT>
-__device__ __forceinline__ uint32_t cw_coop_len(const CwLds<HeadT> &L, uint32_t p, uint32_t r,
+template <typename HeadT, bool WRAP>
+__device__ __forceinline__ uint32_t cw_coop_len(const CwLds<HeadT, WRAP> &L, uint32_t p, uint32_t r,
                                                 uint32_t k0, uint32_t lim)
 {
     const uint32_t lane = threadIdx.x;
@@ -225,15 +228,15 @@ __device__ __forceinline__ uint32_t cw_coop_len(const CwLds<HeadT> &L, uint32_t 
 /* Latest inserted position < P with slot s (or none), from the bucket head
  * hv and the skip chain; exactly the reference's table entry when it is
  * within the 8 KiB window (src/lzf_c.c:147-155). */
-template <typename HeadT>
-__device__ __forceinline__ uint32_t cw_lookup(const CwLds<HeadT> &L, HeadT hv, uint32_t s, uint32_t p)
+template <typename HeadT, bool WRAP>
+__device__ __forceinline__ uint32_t cw_lookup(const CwLds<HeadT, WRAP> &L, HeadT hv, uint32_t s, uint32_t p)
 {
     typedef HeadOps<HeadT> H;
     if (hv == H::NONE) return 0xFFFFFFFFu;
     uint32_t q = H::pos(hv), sq = H::slot(hv);
     while (p - q <= LZF_WINDOW) {
         if (sq == s) return q;
-        const uint32_t d = L.chain[q & L.cmask];      /* skip q's run of its slot */
+        const uint32_t d = L.chain[L.ci(q)];      /* skip q's run of its slot */
         if (d == 0u) break;
         q -= d;
         sq = slot_of(L.rd4(q) & 0xFFFFFFu);
@@ -243,18 +246,17 @@ __device__ __forceinline__ uint32_t cw_lookup(const CwLds<HeadT> &L, HeadT hv, u
 
 /* First mismatch index in [3, kc) of p vs r (kc <= 19), or kc: five aligned
  * dwords per side, no loop. */
-template <typename HeadT>
-__device__ __forceinline__ uint32_t cw_probe(const CwLds<HeadT> &L, uint32_t p, uint32_t r, uint32_t kc)
+template <typename HeadT, bool WRAP>
+__device__ __forceinline__ uint32_t cw_probe(const CwLds<HeadT, WRAP> &L, uint32_t p, uint32_t r, uint32_t kc)
 {
     const uint32_t *w = (const uint32_t *)L.ring;
-    const uint32_t wm = L.rmask >> 2;
     const uint32_t pa = (p + 3u) >> 2, ra = (r + 3u) >> 2;
     const uint32_t ps = (p + 3u) & 3u, rs = (r + 3u) & 3u;
     uint32_t pw[5], rw[5];
 #pragma unroll
     for (int t = 0; t < 5; t++) {
-        pw[t] = w[(pa + t) & wm];
-        rw[t] = w[(ra + t) & wm];
+        pw[t] = w[L.wi(pa + t)];
+        rw[t] = w[L.wi(ra + t)];
     }
     uint32_t k = kc;
 #pragma unroll
@@ -295,12 +297,12 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, uint32_t l)
     return ((uint64_t)readlane_u32((uint32_t)(v >> 32), l) << 32) | readlane_u32((uint32_t)v, l);
 }
 
-template <typename HeadT>
+template <typename HeadT, bool WRAP>
 __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, uint32_t ring_bytes)
 {
     typedef HeadOps<HeadT> H;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    CwLds<HeadT> L;
+    CwLds<HeadT, WRAP> L;
     L.ring = smem;
     L.rmask = ring_bytes - 1u;
     uint8_t *cur = smem + ring_bytes;
@@ -398,7 +400,7 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
 
         /* ---- 2. exact table lookup among positions < P --------------- */
         uint32_t T = 0xFFFFFFFFu;
-        if (valid && prevW < 0) T = cw_lookup<HeadT>(L, hv, s, p);
+        if (valid && prevW < 0) T = cw_lookup<HeadT, WRAP>(L, hv, s, p);
         CW_PHASE(3);
 
         /* ---- 3. match test (src/lzf_c.c:151-166), probed length ------ */
@@ -460,11 +462,10 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
             }
             end = exitLane >= 0 ? (uint32_t)exitLane + 1u : lim_lane;
             /* visited = not strictly inside the reach of an earlier orbit match */
+            /* (orbit match lanes are visited; their own reach is > lane) */
             const uint32_t reach = ((MMV >> lane) & 1ull) ? lane + m : 0u;
-            uint32_t before = (uint32_t)__shfl_up((int)reach, 1);
-            if (lane == 0) before = 0u;
-            const uint32_t rmax = cd_incl_max(before);
-            V = __ballot(rmax <= lane) & lanemask_lt(end);
+            const uint32_t rmax = cd_incl_max(reach);
+            V = (__ballot(rmax <= lane) | MMV) & lanemask_lt(end);
             /* speculation check: prevW must be an inserted position */
             const uint64_t INTR = ~V & ~(V >> 1) & ~(V >> 2);    /* inside a match */
             const bool vis = (V >> lane) & 1ull;
@@ -483,7 +484,7 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
                 HeadT hf;
                 if constexpr (sizeof(HeadT) == 8) hf = (HeadT)readlane_u64((uint64_t)hv, f);
                 else hf = (HeadT)readlane_u32((uint32_t)hv, f);
-                rf = cw_lookup<HeadT>(L, hf, readlane_u32(s, f), pf);
+                rf = cw_lookup<HeadT, WRAP>(L, hf, readlane_u32(s, f), pf);
             }
             bool ok = rf != 0xFFFFFFFFu && rf > 0u && (pf - rf - 1u) < LZF_WINDOW && pf + 4u < n;
             if (ok) ok = readlane_u32(L.rd4(rf) & 0xFFFFFFu, 0) == readlane_u32(tri, f);
@@ -585,9 +586,9 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
             } else if (hv != H::NONE && p - H::pos(hv) <= LZF_WINDOW) {
                 const uint32_t hp = H::pos(hv);
                 if (H::slot(hv) != s) y = hp;
-                else if (L.chain[hp & L.cmask]) y = hp - L.chain[hp & L.cmask];
+                else if (L.chain[L.ci(hp)]) y = hp - L.chain[L.ci(hp)];
             }
-            L.chain[p & L.cmask] = (uint16_t)((y != 0xFFFFFFFFu && p - y <= LZF_WINDOW) ? p - y : 0u);
+            L.chain[L.ci(p)] = (uint16_t)((y != 0xFFFFFFFFu && p - y <= LZF_WINDOW) ? p - y : 0u);
             if (last) L.head[b] = H::make(s, p);
         }
         wave_lds_fence();
@@ -641,25 +642,26 @@ static uint32_t ring_for(uint32_t max_len)
     return r;
 }
 
-template <typename HeadT>
+template <typename HeadT, bool WRAP>
 static hipError_t launch_window(const LzfBatch &b, hipStream_t s)
 {
     const uint32_t ring = ring_for(b.max_len);
     const uint32_t chain = ring < CW_CHAIN ? ring : CW_CHAIN;
     const size_t lds = ring + CW_HBUCKETS * sizeof(HeadT) + CW_TALL * 8u +
                        chain * sizeof(uint16_t);
-    hipError_t e = hipFuncSetAttribute((const void *)lzf_compress_window_kernel<HeadT>,
+    hipError_t e = hipFuncSetAttribute((const void *)lzf_compress_window_kernel<HeadT, WRAP>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(lzf_compress_window_kernel<HeadT>, dim3(b.count), dim3(CW_LANES), lds, s, b,
-                       ring);
+    lzf_compress_window_kernel<HeadT, WRAP><<<dim3(b.count), dim3(CW_LANES), lds, s>>>(b, ring);
     return hipGetLastError();
 }
 
 hipError_t lzf_launch_compress(const LzfBatch &b, hipStream_t s)
 {
-    if (b.max_len <= 65536u) return launch_window<uint32_t>(b, s);
-    return launch_window<unsigned long long>(b, s);
+    /* values that fit the chain (8 KiB) never wrap the ring or the chain */
+    if (b.max_len <= CW_CHAIN) return launch_window<uint32_t, false>(b, s);
+    if (b.max_len <= 65536u) return launch_window<uint32_t, true>(b, s);
+    return launch_window<unsigned long long, true>(b, s);
 }
 
 const char *lzf_compress_kernel_name(void) { return "window64"; }
