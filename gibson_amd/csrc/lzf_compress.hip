@@ -111,23 +111,29 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x)
     return x;
 }
 
-/* Bucket-head entry: slot and position of the latest inserted position of
- * the bucket.  Values up to 64 KiB pack both into 32 bits. */
+/* Bucket-head entry: position of the latest inserted position of the
+ * bucket, its slot's identity within the bucket (slot-mix bits 0-5; the
+ * bucket fixes the rest) and an 8-bit presence filter over the identities
+ * ever inserted into the bucket (bit ident & 7).  A lookup whose filter bit
+ * is clear has no same-slot entry to find and skips the chain walk.  Values
+ * up to 64 KiB use 32-bit entries [pos:16 | ident:8 | filter:8]; longer
+ * ones 64-bit [pos:32 | ident:8 | filter:8 | 0:16]. */
 template <typename E> struct HeadOps;
 template <> struct HeadOps<uint32_t> {
-    static constexpr uint32_t NONE = 0xFFFFFFFFu;
-    __device__ static uint32_t make(uint32_t s, uint32_t p) { return (s << 16) | (p & 0xFFFFu); }
+    typedef uint16_t PosT;
+    static constexpr uint32_t EMPTY = 0x00FFFFFFu;      /* no position, empty filter */
     __device__ static uint32_t pos(uint32_t e) { return e & 0xFFFFu; }
-    __device__ static uint32_t slot(uint32_t e) { return e >> 16; }
+    __device__ static bool empty(uint32_t e) { return (e & 0xFFFFu) == 0xFFFFu; }
+    __device__ static uint32_t ident(uint32_t e) { return (e >> 16) & 0xFFu; }
+    __device__ static uint32_t filter(uint32_t e) { return e >> 24; }
 };
 template <> struct HeadOps<unsigned long long> {
-    static constexpr unsigned long long NONE = ~0ull;
-    __device__ static unsigned long long make(uint32_t s, uint32_t p)
-    {
-        return ((unsigned long long)s << 32) | p;
-    }
+    typedef uint32_t PosT;
+    static constexpr unsigned long long EMPTY = 0x000000FFFFFFFFFFull;
     __device__ static uint32_t pos(unsigned long long e) { return (uint32_t)e; }
-    __device__ static uint32_t slot(unsigned long long e) { return (uint32_t)(e >> 32); }
+    __device__ static bool empty(unsigned long long e) { return (uint32_t)e == 0xFFFFFFFFu; }
+    __device__ static uint32_t ident(unsigned long long e) { return (uint32_t)(e >> 32) & 0xFFu; }
+    __device__ static uint32_t filter(unsigned long long e) { return (uint32_t)(e >> 40) & 0xFFu; }
 };
 
 template <typename HeadT, bool WRAP>
@@ -179,22 +185,41 @@ __device__ void cw_fill(const CwLds<HeadT, WRAP> &L, const uint8_t *src, uint32_
 
 __device__ __forceinline__ uint32_t slot_mix(uint32_t s) { return (s * 40503u) & 0xFFFFu; }
 __device__ __forceinline__ uint32_t bucket_of(uint32_t sm) { return sm >> (16 - CW_HBITS); }
+__device__ __forceinline__ uint32_t ident_of(uint32_t sm) { return sm & (CW_T1 - 1u); }
+__device__ __forceinline__ uint32_t filter_bit(uint32_t id) { return 1u << (id & 7u); }
+
+/* Bucket-head updates.  The filter bit is OR-ed in (every inserted position);
+ * position and identity are plain sub-word stores (the bucket's last one). */
+template <typename HeadT>
+__device__ __forceinline__ void head_mark(HeadT *head, uint32_t b, uint32_t id)
+{
+    uint32_t *w = (uint32_t *)(head + b) + (sizeof(HeadT) == 8 ? 1 : 0);
+    atomicOr(w, filter_bit(id) << (sizeof(HeadT) == 8 ? 8 : 24));
+}
+template <typename HeadT>
+__device__ __forceinline__ void head_set(HeadT *head, uint32_t b, uint32_t id, uint32_t x)
+{
+    typedef typename HeadOps<HeadT>::PosT PosT;
+    *(PosT *)(head + b) = (PosT)x;
+    *((uint8_t *)(head + b) + sizeof(PosT)) = (uint8_t)id;
+}
 
 /* Insert position x (slot sx) after every earlier position (one lane). */
 template <typename HeadT, bool WRAP>
 __device__ __forceinline__ void cw_insert_one(const CwLds<HeadT, WRAP> &L, uint32_t x, uint32_t sx)
 {
     typedef HeadOps<HeadT> H;
-    const uint32_t bx = bucket_of(slot_mix(sx));
+    const uint32_t smx = slot_mix(sx), bx = bucket_of(smx), idx = ident_of(smx);
     const HeadT hv = L.head[bx];
     uint32_t y = 0xFFFFFFFFu;
-    if (hv != H::NONE && x - H::pos(hv) <= LZF_WINDOW) {
+    if (!H::empty(hv) && x - H::pos(hv) <= LZF_WINDOW) {
         const uint32_t hp = H::pos(hv);
-        if (H::slot(hv) != sx) y = hp;
+        if (H::ident(hv) != idx) y = hp;
         else if (L.chain[L.ci(hp)]) y = hp - L.chain[L.ci(hp)];
     }
     L.chain[L.ci(x)] = (uint16_t)((y != 0xFFFFFFFFu && x - y <= LZF_WINDOW) ? x - y : 0u);
-    L.head[bx] = H::make(sx, x);
+    head_mark(L.head, bx, idx);
+    head_set(L.head, bx, idx, x);
 }
 
 /* Length of the match p/r whose first k0 bytes are known equal, up to lim:
@@ -227,19 +252,23 @@ __device__ __forceinline__ uint32_t cw_coop_len(const CwLds<HeadT, WRAP> &L, uin
 
 /* Latest inserted position < P with slot s (or none), from the bucket head
  * hv and the skip chain; exactly the reference's table entry when it is
- * within the 8 KiB window (src/lzf_c.c:147-155). */
+ * within the 8 KiB window (src/lzf_c.c:147-155).  id = s's identity in its
+ * bucket; a clear filter bit means s was never inserted. */
 template <typename HeadT, bool WRAP>
-__device__ __forceinline__ uint32_t cw_lookup(const CwLds<HeadT, WRAP> &L, HeadT hv, uint32_t s, uint32_t p)
+__device__ __forceinline__ uint32_t cw_lookup(const CwLds<HeadT, WRAP> &L, HeadT hv, uint32_t hch, uint32_t s,
+                                              uint32_t id, uint32_t p)
 {
     typedef HeadOps<HeadT> H;
-    if (hv == H::NONE) return 0xFFFFFFFFu;
-    uint32_t q = H::pos(hv), sq = H::slot(hv);
+    if (!(H::filter(hv) & filter_bit(id))) return 0xFFFFFFFFu;   /* never inserted (or empty) */
+    uint32_t q = H::pos(hv);
+    bool same = H::ident(hv) == id;
+    uint32_t d = hch;                             /* the head's chain entry, read early */
     while (p - q <= LZF_WINDOW) {
-        if (sq == s) return q;
-        const uint32_t d = L.chain[L.ci(q)];      /* skip q's run of its slot */
-        if (d == 0u) break;
+        if (same) return q;
+        if (d == 0u) break;                       /* skip q's run of its slot */
         q -= d;
-        sq = slot_of(L.rd4(q) & 0xFFFFFFu);
+        same = slot_of(L.rd4(q) & 0xFFFFFFu) == s;
+        d = L.chain[L.ci(q)];
     }
     return 0xFFFFFFFFu;
 }
@@ -331,10 +360,9 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
     }
 
     {
-        uint32_t *z = (uint32_t *)L.head;   /* heads = NONE, bitmaps = 0 */
-        const uint32_t nh = CW_HBUCKETS * sizeof(HeadT) / 4u;
-        for (uint32_t k = lane; k < nh; k += CW_LANES) z[k] = ~0u;
-        for (uint32_t k = lane; k < CW_TALL * 2u; k += CW_LANES) z[nh + k] = 0u;
+        for (uint32_t k = lane; k < CW_HBUCKETS; k += CW_LANES) L.head[k] = H::EMPTY;
+        uint32_t *z = (uint32_t *)(L.head + CW_HBUCKETS);      /* lane bitmaps = 0 */
+        for (uint32_t k = lane; k < CW_TALL * 2u; k += CW_LANES) z[k] = 0u;
     }
     uint32_t loaded = n < ring_bytes ? n : ring_bytes;
     cw_fill(L, src, 0u, loaded);
@@ -372,19 +400,21 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
         const uint32_t b = bucket_of(sm);
         const uint32_t k1 = sm & (CW_T1 - 1u), k2 = (sm >> (16 - CW_HBITS)) & (CW_T2 - 1u), k3 = sm >> 12;
         const unsigned long long me = 1ull << lane;
+        HeadT hv = H::EMPTY;
         if (valid) {
             atomicOr(&L.t1[k1], me);
             atomicOr(&L.t2[k2], me);
             atomicOr(&L.t3[k3], me);
+            hv = L.head[b];
         }
         wave_lds_fence();
         uint64_t M1 = 0, M2 = 0, M3 = 0;
-        HeadT hv = H::NONE;
+        uint32_t hch = 0;                         /* chain entry of the bucket head */
         if (valid) {
             M1 = L.t1[k1];
             M2 = L.t2[k2];
             M3 = L.t3[k3];
-            hv = L.head[b];
+            if (!H::empty(hv)) hch = L.chain[L.ci(H::pos(hv))];
         }
         wave_lds_fence();
         if (valid) {
@@ -400,7 +430,7 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
 
         /* ---- 2. exact table lookup among positions < P --------------- */
         uint32_t T = 0xFFFFFFFFu;
-        if (valid && prevW < 0) T = cw_lookup<HeadT, WRAP>(L, hv, s, p);
+        if (valid && prevW < 0) T = cw_lookup<HeadT, WRAP>(L, hv, hch, s, k1, p);
         CW_PHASE(3);
 
         /* ---- 3. match test (src/lzf_c.c:151-166), probed length ------ */
@@ -484,7 +514,8 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
                 HeadT hf;
                 if constexpr (sizeof(HeadT) == 8) hf = (HeadT)readlane_u64((uint64_t)hv, f);
                 else hf = (HeadT)readlane_u32((uint32_t)hv, f);
-                rf = cw_lookup<HeadT, WRAP>(L, hf, readlane_u32(s, f), pf);
+                rf = cw_lookup<HeadT, WRAP>(L, hf, readlane_u32(hch, f), readlane_u32(s, f),
+                                            readlane_u32(k1, f), pf);
             }
             bool ok = rf != 0xFFFFFFFFu && rf > 0u && (pf - rf - 1u) < LZF_WINDOW && pf + 4u < n;
             if (ok) ok = readlane_u32(L.rd4(rf) & 0xFFFFFFu, 0) == readlane_u32(tri, f);
@@ -583,19 +614,20 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
             uint32_t y = 0xFFFFFFFFu;
             if (other) {
                 y = P + 63u - (uint32_t)__builtin_clzll(other);
-            } else if (hv != H::NONE && p - H::pos(hv) <= LZF_WINDOW) {
+            } else if (!H::empty(hv) && p - H::pos(hv) <= LZF_WINDOW) {
                 const uint32_t hp = H::pos(hv);
-                if (H::slot(hv) != s) y = hp;
-                else if (L.chain[L.ci(hp)]) y = hp - L.chain[L.ci(hp)];
+                if (H::ident(hv) != k1) y = hp;
+                else if (hch) y = hp - hch;
             }
             L.chain[L.ci(p)] = (uint16_t)((y != 0xFFFFFFFFu && p - y <= LZF_WINDOW) ? p - y : 0u);
-            if (last) L.head[b] = H::make(s, p);
+            head_mark(L.head, b, k1);
+            if (last) head_set(L.head, b, k1, p);
         }
         wave_lds_fence();
         if (tx0 != 0xFFFFFFFFu || tx1 != 0xFFFFFFFFu) {
             if (lane == 0) {
-                if (tx0 != 0xFFFFFFFFu) cw_insert_one(L, tx0, slot_of(L.rd4(tx0) & 0xFFFFFFu));
-                if (tx1 != 0xFFFFFFFFu) cw_insert_one(L, tx1, slot_of(L.rd4(tx1) & 0xFFFFFFu));
+                if (tx0 != 0xFFFFFFFFu) cw_insert_one<HeadT, WRAP>(L, tx0, slot_of(L.rd4(tx0) & 0xFFFFFFu));
+                if (tx1 != 0xFFFFFFFFu) cw_insert_one<HeadT, WRAP>(L, tx1, slot_of(L.rd4(tx1) & 0xFFFFFFu));
             }
             wave_lds_fence();
         }
@@ -603,9 +635,9 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
         P = Pn;
     }
 #ifdef LZF_CW_STATS
-    atomicAdd(&cw_stats[ST_HOPS], st_hops);
-    atomicAdd(&cw_stats[ST_EXT], st_ext);
     if (lane == 0) {
+        atomicAdd(&cw_stats[ST_HOPS], st_hops);
+        atomicAdd(&cw_stats[ST_EXT], st_ext);
         atomicAdd(&cw_stats[ST_WINDOWS], st_windows);
         atomicAdd(&cw_stats[ST_TRUNC], st_trunc);
         atomicAdd(&cw_stats[ST_ORBITM], st_orbitm);

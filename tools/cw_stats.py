@@ -43,7 +43,7 @@ def main():
     print(f"kind {kind} n {n} count {count}: {e0.elapsed_time(e1):.2f} ms, "
           f"{count * n / e0.elapsed_time(e1) / 1e6:.2f} GB/s, ratio {float(ol.sum()) / (count * n):.4f}")
     print(f"windows/value {st[0] / vals:.1f}  repairs/value {st[1] / vals:.2f}  "
-          f"hops/window {st[2] / w:.1f}  ext-iters/window {st[3] / w:.1f}  "
+          f"unfinished-lookups/window {st[3] / w:.2f}  resolved-on-orbit/window {st[2] / w:.2f}  "
           f"orbit-matches/window {st[4] / w:.2f}  coop/window {st[6] / w:.2f}")
     tot = sum(st[8:8 + len(PHASES)])
     for i, name in enumerate(PHASES):
