@@ -56,6 +56,7 @@
 #define CW_CHAIN     8192u
 #define CW_RING_MAX  16384u
 #define CW_EXT_CAP   19u          /* per-lane match length probe (3 + 4 x 4 bytes) */
+#define CW_TBYTES    (CW_TALL * 8u)
 
 /* Diagnostic build only (make stats -> liblzf_hip_stats.so): per-phase
  * s_memtime cycles and event counts, summed over all waves. */
@@ -336,9 +337,10 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
     L.rmask = ring_bytes - 1u;
     uint8_t *cur = smem + ring_bytes;
     L.head = (HeadT *)cur;                   cur += CW_HBUCKETS * sizeof(HeadT);
-    L.t1 = (unsigned long long *)cur;        cur += CW_T1 * 8u;
-    L.t2 = (unsigned long long *)cur;        cur += CW_T2 * 8u;
-    L.t3 = (unsigned long long *)cur;        cur += CW_T3 * 8u;
+    L.t1 = (unsigned long long *)cur;
+    L.t2 = L.t1 + CW_T1;
+    L.t3 = L.t2 + CW_T2;
+    cur += CW_TBYTES;
     L.chain = (uint16_t *)cur;
     L.cmask = (ring_bytes < CW_CHAIN ? ring_bytes : CW_CHAIN) - 1u;
 
@@ -362,7 +364,7 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
     {
         for (uint32_t k = lane; k < CW_HBUCKETS; k += CW_LANES) L.head[k] = H::EMPTY;
         uint32_t *z = (uint32_t *)(L.head + CW_HBUCKETS);      /* lane bitmaps = 0 */
-        for (uint32_t k = lane; k < CW_TALL * 2u; k += CW_LANES) z[k] = 0u;
+        for (uint32_t k = lane; k < CW_TBYTES / 4u; k += CW_LANES) z[k] = 0u;
     }
     uint32_t loaded = n < ring_bytes ? n : ring_bytes;
     cw_fill(L, src, 0u, loaded);
@@ -398,18 +400,19 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
         const uint32_t s = slot_of(tri);
         const uint32_t sm = slot_mix(s);          /* bijective 16-bit mix of the slot */
         const uint32_t b = bucket_of(sm);
-        const uint32_t k1 = sm & (CW_T1 - 1u), k2 = (sm >> (16 - CW_HBITS)) & (CW_T2 - 1u), k3 = sm >> 12;
-        const unsigned long long me = 1ull << lane;
+        const uint32_t k1 = ident_of(sm);
         HeadT hv = H::EMPTY;
+        uint32_t hch = 0;                         /* chain entry of the bucket head */
+        if (valid) hv = L.head[b];
+        const uint32_t k2 = (sm >> (16 - CW_HBITS)) & (CW_T2 - 1u), k3 = sm >> 12;
+        const unsigned long long me = 1ull << lane;
         if (valid) {
             atomicOr(&L.t1[k1], me);
             atomicOr(&L.t2[k2], me);
             atomicOr(&L.t3[k3], me);
-            hv = L.head[b];
         }
         wave_lds_fence();
         uint64_t M1 = 0, M2 = 0, M3 = 0;
-        uint32_t hch = 0;                         /* chain entry of the bucket head */
         if (valid) {
             M1 = L.t1[k1];
             M2 = L.t2[k2];
@@ -679,7 +682,7 @@ static hipError_t launch_window(const LzfBatch &b, hipStream_t s)
 {
     const uint32_t ring = ring_for(b.max_len);
     const uint32_t chain = ring < CW_CHAIN ? ring : CW_CHAIN;
-    const size_t lds = ring + CW_HBUCKETS * sizeof(HeadT) + CW_TALL * 8u +
+    const size_t lds = ring + CW_HBUCKETS * sizeof(HeadT) + CW_TBYTES +
                        chain * sizeof(uint16_t);
     hipError_t e = hipFuncSetAttribute((const void *)lzf_compress_window_kernel<HeadT, WRAP>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -103,13 +103,16 @@ def test_batch_decompress_serial_generation(golden, oracle, monkeypatch):
     test_batch_decompress_golden(golden, oracle)
 
 
-def test_random_differential(oracle, generation):
+@pytest.mark.parametrize("nmax", [8192, 9000])
+def test_random_differential(oracle, generation, nmax):
+    # nmax 8192: the batch fits the non-wrapping ring/chain kernel; 9000:
+    # the wrapping one (the kernel is chosen per batch from max_len)
     from tests.gpu_batch import gpu_compress, gpu_decompress
-    rnd = random.Random(7)
+    rnd = random.Random(7 + nmax)
     vals, caps = [], []
     for it in range(3000):
         kind = rnd.randrange(6)
-        n = rnd.choice([rnd.randint(1, 64), rnd.randint(1, 700), rnd.randint(1, 9000)])
+        n = rnd.choice([rnd.randint(1, 64), rnd.randint(1, 700), rnd.randint(1, nmax)])
         v = synth(kind, rnd.getrandbits(32), it, n)
         if rnd.random() < 0.2:
             v = bytes(rnd.choice(b"ab") for _ in range(n))
@@ -140,6 +143,29 @@ def test_edge_cases(oracle):
             # phantom control byte 0xff for the empty stream, as in tests/golden
             o, e = oracle.decompress(s, cap)
             assert d == (o, e), (s, cap, d, (o, e))
+
+
+def test_large_values(oracle, generation):
+    # values past the 16 KiB ring (wrapping ring and chain) and past 64 KiB
+    # (64-bit bucket heads), up to 1 MiB
+    from tests.gpu_batch import gpu_compress, gpu_decompress
+    if generation == "serial":
+        pytest.skip("the serial kernel is limited to 64 KiB")
+    rnd = random.Random(11)
+    vals, caps = [], []
+    for k, n in enumerate([16385, 70000, 65537, 200003, 1 << 20]):
+        v = synth(k % 6, 0x5EED00AA, k, n)
+        if k == 3:
+            v = bytes(rnd.choice(b"abc") for _ in range(n))
+        vals.append(v)
+        caps.append(n - 4)
+    res = gpu_compress(vals, caps)
+    for v, c, r in zip(vals, caps, res):
+        assert r == oracle.compress(v, c), len(v)
+    streams = [r for r in res if r]
+    origs = [v for v, r in zip(vals, res) if r]
+    assert streams
+    assert gpu_decompress(streams, [len(v) for v in origs]) == [(v, 0) for v in origs]
 
 
 def test_device_generator_matches_host():
