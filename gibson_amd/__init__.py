@@ -8,7 +8,12 @@ src/lzf.h:76-97) plus device-batch helpers over torch tensors (torch is only
 device-memory and stream plumbing here).
 """
 from .lzf import (  # noqa: F401
+    ENC_LZF,
+    ENC_NULL,
+    ENC_NUMBER,
+    ENC_PLAIN,
     LZF_VERSION,
+    REPL_KVAL,
     LzfLibraryMissing,
     compress_batch,
     decompress_batch,
@@ -20,4 +25,5 @@ from .lzf import (  # noqa: F401
     synth_fill,
     host_compress_batch,
     host_decompress_batch,
+    kv_frame,
 )

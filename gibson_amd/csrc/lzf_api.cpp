@@ -197,7 +197,7 @@ int host_batch(bool compress, const uint8_t *in, const uint64_t *in_off, const u
     size_t res_off = (uint8_t *)m_out_len - h_meta;
     check(hipMemcpyAsync(d_in, h_in, in_end, hipMemcpyHostToDevice, c.stream), "hipMemcpyAsync");
     check(hipMemcpyAsync(d_meta, h_meta, res_off, hipMemcpyHostToDevice, c.stream), "hipMemcpyAsync");
-    LzfBatch b;
+    LzfBatch b{};
     b.in = d_in;
     b.in_off = (const uint64_t *)d_meta;
     b.out_off = b.in_off + count;
@@ -309,6 +309,37 @@ int lzf_host_decompress_batch(const uint8_t *in, const uint64_t *in_off, const u
                               uint32_t *out_len, int32_t *err, uint32_t count)
 {
     return host_batch(false, in, in_off, in_len, out, out_off, out_cap, out_len, err, count);
+}
+
+uint64_t lzf_gpu_kv_frame_work_size(uint32_t count)
+{
+    return lzf_frame_work_bytes(count);
+}
+
+int lzf_gpu_kv_frame(const uint8_t *keys, const uint64_t *key_off, const uint32_t *key_len,
+                     const uint8_t *vals, const uint64_t *val_off, const uint32_t *val_size,
+                     const uint8_t *enc, const uint32_t *val_len, uint32_t count,
+                     uint32_t elements, uint32_t max_val_len, int reply_header,
+                     uint8_t *frame, uint64_t max_response, uint64_t *frame_len, void *work,
+                     void *stream)
+{
+    if (!count || !keys || !key_off || !key_len || !vals || !val_off || !val_size || !enc ||
+        !val_len || !frame || !frame_len || !work)
+        return LZF_GPU_EARG;
+    if (max_val_len > LZF_GPU_MAX_VALUE) return LZF_GPU_EARG;
+    int rc = current_device_ok();
+    if (rc) return rc;
+    LzfFrameArgs a{};
+    a.keys = keys; a.key_off = key_off; a.key_len = key_len;
+    a.vals = vals; a.val_off = val_off; a.val_size = val_size;
+    a.enc = enc; a.val_len = val_len;
+    a.count = count; a.elements = elements; a.max_val_len = max_val_len ? max_val_len : 1u;
+    a.reply_header = reply_header;
+    a.max_response = max_response;
+    a.frame = frame; a.frame_len = frame_len;
+    lzf_frame_carve(a, work);
+    return lzf_launch_frame(a, (hipStream_t)stream, launch_decompress) == hipSuccess ? LZF_GPU_OK
+                                                                                    : LZF_GPU_ELAUNCH;
 }
 
 const char *lzf_gpu_kernel_info(void)

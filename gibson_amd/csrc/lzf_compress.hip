@@ -205,24 +205,6 @@ __device__ __forceinline__ void head_set(HeadT *head, uint32_t b, uint32_t id, u
     *((uint8_t *)(head + b) + sizeof(PosT)) = (uint8_t)id;
 }
 
-/* Insert position x (slot sx) after every earlier position (one lane). */
-template <typename HeadT, bool WRAP>
-__device__ __forceinline__ void cw_insert_one(const CwLds<HeadT, WRAP> &L, uint32_t x, uint32_t sx)
-{
-    typedef HeadOps<HeadT> H;
-    const uint32_t smx = slot_mix(sx), bx = bucket_of(smx), idx = ident_of(smx);
-    const HeadT hv = L.head[bx];
-    uint32_t y = 0xFFFFFFFFu;
-    if (!H::empty(hv) && x - H::pos(hv) <= LZF_WINDOW) {
-        const uint32_t hp = H::pos(hv);
-        if (H::ident(hv) != idx) y = hp;
-        else if (L.chain[L.ci(hp)]) y = hp - L.chain[L.ci(hp)];
-    }
-    L.chain[L.ci(x)] = (uint16_t)((y != 0xFFFFFFFFu && x - y <= LZF_WINDOW) ? x - y : 0u);
-    head_mark(L.head, bx, idx);
-    head_set(L.head, bx, idx, x);
-}
-
 /* Length of the match p/r whose first k0 bytes are known equal, up to lim:
  * the whole wave compares 256 bytes per step (uniform inputs and result). */
 template <typename HeadT, bool WRAP>
@@ -554,34 +536,29 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
         const uint32_t delta = (visited && isM) ? Tr + tlen : 0u;
         const uint32_t incl = wave_incl_sum(delta);
         const uint32_t myH0 = H0 + incl - delta;
-        bool lfail = false;
-        if (visited) {
-            if (!isM) {
-                const uint32_t pos = myH0 + nf;
-                if (pos >= cap) {
-                    lfail = true;                                   /* src/lzf_c.c:263 */
-                } else {
-                    dst[pos] = (uint8_t)L.rd1(p);
-                    if ((R & 31u) == 31u) dst[pos - 32u] = 31u;     /* rollover header */
-                }
-            } else {
-                const uint32_t Tp = myH0 + Tr;
-                if (Tp + 4u >= cap) {
-                    lfail = true;                                   /* src/lzf_c.c:176 */
-                } else {
-                    if (R & 31u) dst[myH0 + 33u * (R >> 5)] = (uint8_t)((R & 31u) - 1u);
-                    const uint32_t off = p - ref - 1u;
-                    const uint32_t Lc = m - 2u;
-                    if (Lc < 7u) {
-                        dst[Tp] = (uint8_t)((off >> 8) | (Lc << 5));
-                        dst[Tp + 1u] = (uint8_t)off;
-                    } else {
-                        dst[Tp] = (uint8_t)((off >> 8) | 0xE0u);
-                        dst[Tp + 1u] = (uint8_t)(Lc - 7u);
-                        dst[Tp + 2u] = (uint8_t)off;
-                    }
-                }
-            }
+        /* Each visited lane stores up to four bytes, as four unconditional
+         * stores under one exec mask: an unused store repeats the lane's
+         * previous (address, byte).  Literal: [rollover header 31 at pos-32]
+         * + the byte.  Match: [run header] + 2 or 3 back-reference bytes.
+         * Out of space (src/lzf_c.c:176, 263): nothing of the lane is stored. */
+        const uint32_t off = p - ref - 1u;
+        const uint32_t Lc = m - 2u;
+        const uint32_t pos = myH0 + (isM ? Tr : nf);
+        const bool lfail = visited && (isM ? pos + 4u >= cap : pos >= cap);
+        const uint32_t b0 = isM ? ((off >> 8) | (Lc < 7u ? Lc << 5 : 0xE0u)) : L.rd1(p);
+        const bool h1 = isM ? (R & 31u) != 0u : (R & 31u) == 31u;
+        const uint32_t a1 = h1 ? (isM ? myH0 + 33u * (R >> 5) : pos - 32u) : pos;
+        const uint32_t v1 = h1 ? (isM ? (R & 31u) - 1u : 31u) : b0;
+        const uint32_t a3 = isM ? pos + 1u : pos;
+        const uint32_t v3 = isM ? (Lc < 7u ? off : Lc - 7u) : b0;
+        const bool long3 = isM && Lc >= 7u;
+        const uint32_t a4 = long3 ? pos + 2u : a3;
+        const uint32_t v4 = long3 ? off : v3;
+        if (visited && !lfail) {
+            dst[a1] = (uint8_t)v1;
+            dst[pos] = (uint8_t)b0;
+            dst[a3] = (uint8_t)v3;
+            dst[a4] = (uint8_t)v4;
         }
         if (__ballot(lfail)) { fail = true; break; }
         CW_PHASE(6);
@@ -628,9 +605,34 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
         }
         wave_lds_fence();
         if (tx0 != 0xFFFFFFFFu || tx1 != 0xFFFFFFFFu) {
-            if (lane == 0) {
-                if (tx0 != 0xFFFFFFFFu) cw_insert_one<HeadT, WRAP>(L, tx0, slot_of(L.rd4(tx0) & 0xFFFFFFu));
-                if (tx1 != 0xFFFFFFFFu) cw_insert_one<HeadT, WRAP>(L, tx1, slot_of(L.rd4(tx1) & 0xFFFFFFu));
+            /* the exit match's tails past the window: lane 0 inserts tx0,
+             * lane 1 tx1 (after tx0: when both hit one bucket, tx0 is tx1's
+             * head) */
+            const uint32_t t = lane == 0 ? tx0 : tx1;
+            const bool act = lane < 2u && t != 0xFFFFFFFFu;
+            uint32_t bt = 0xFFFFFFFFu, idt = 0, y = 0xFFFFFFFFu;
+            if (act) {
+                const uint32_t smt = slot_mix(slot_of(L.rd4(t) & 0xFFFFFFu));
+                bt = bucket_of(smt);
+                idt = ident_of(smt);
+                const HeadT ht = L.head[bt];
+                if (!H::empty(ht) && t - H::pos(ht) <= LZF_WINDOW) {
+                    const uint32_t hp = H::pos(ht);
+                    if (H::ident(ht) != idt) {
+                        y = hp;
+                    } else {
+                        const uint32_t d = L.chain[L.ci(hp)];
+                        if (d) y = hp - d;
+                    }
+                }
+            }
+            const uint32_t b0t = readlane_u32(bt, 0), b1t = readlane_u32(bt, 1);
+            const uint32_t id0 = readlane_u32(idt, 0), y0 = readlane_u32(y, 0);
+            if (lane == 1 && tx0 != 0xFFFFFFFFu && bt == b0t) y = id0 != idt ? tx0 : y0;
+            if (act) {
+                L.chain[L.ci(t)] = (uint16_t)((y != 0xFFFFFFFFu && t - y <= LZF_WINDOW) ? t - y : 0u);
+                head_mark(L.head, bt, idt);
+                if (lane == 1 || tx1 == 0xFFFFFFFFu || b1t != bt) head_set(L.head, bt, idt, t);
             }
             wave_lds_fence();
         }

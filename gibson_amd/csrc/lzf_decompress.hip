@@ -80,6 +80,7 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
 
     const uint32_t lane = threadIdx.x;
     const uint32_t v = blockIdx.x;
+    if (bt.skip && bt.skip[v]) return;
     const uint32_t in_len = bt.in_len[v];
     const uint32_t cap = bt.out_cap[v];
     const uint8_t *src = bt.in + bt.in_off[v];

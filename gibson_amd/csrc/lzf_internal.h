@@ -27,6 +27,30 @@ struct LzfBatch {
     int32_t *err;          /* decompress only */
     uint32_t count;
     uint32_t max_len;      /* max in_len (compress) / max out_cap (decompress) */
+    const uint8_t *skip;   /* decompress: values with skip[i] != 0 are left alone (NULL: none) */
+};
+
+/* the MGET reply frame (lzf_frame.hip); device pointers */
+struct LzfFrameArgs {
+    const uint8_t *keys;
+    const uint64_t *key_off;
+    const uint32_t *key_len;
+    const uint8_t *vals;
+    const uint64_t *val_off;
+    const uint32_t *val_size;
+    const uint8_t *enc;
+    const uint32_t *val_len;
+    uint32_t count, elements;
+    uint32_t max_val_len;
+    int reply_header;
+    uint64_t max_response;
+    uint8_t *frame;
+    uint64_t *frame_len;
+    /* work area (lzf_frame_carve) */
+    uint64_t *w_off, *w_voff, *w_bsum, *w_state;
+    uint32_t *w_len;
+    int32_t *w_err;
+    uint8_t *w_skip;
 };
 
 /* launchers, defined next to their kernels; return hipSuccess or the error */
@@ -34,6 +58,10 @@ hipError_t lzf_launch_compress(const LzfBatch &b, hipStream_t s);
 hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s);
 hipError_t lzf_launch_synth(int kind, uint64_t seed, uint64_t first, uint64_t stride,
                             uint32_t count, uint32_t n, uint8_t *out, hipStream_t s);
+hipError_t lzf_launch_frame(LzfFrameArgs &a, hipStream_t s,
+                            hipError_t (*decode)(const LzfBatch &, hipStream_t));
+size_t lzf_frame_work_bytes(uint32_t count);
+void lzf_frame_carve(LzfFrameArgs &a, void *work);
 const char *lzf_compress_kernel_name(void);
 const char *lzf_decompress_kernel_name(void);
 

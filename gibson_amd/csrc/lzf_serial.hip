@@ -102,6 +102,7 @@ __global__ __launch_bounds__(64) void lzf_decompress_serial_kernel(LzfBatch bt)
 {
     if (threadIdx.x != 0) return;
     const uint32_t v = blockIdx.x;
+    if (bt.skip && bt.skip[v]) return;
     const uint8_t *in = bt.in + bt.in_off[v];
     const uint32_t in_len = bt.in_len[v];
     uint8_t *out = bt.out + bt.out_off[v];

@@ -27,7 +27,13 @@ EXPORTS = (
     "lzf_host_compress_batch",
     "lzf_host_decompress_batch",
     "lzf_gpu_kernel_info",
+    "lzf_gpu_kv_frame_work_size",
+    "lzf_gpu_kv_frame",
 )
+
+# item encodings (src/net.h:274-278) and the MGET reply code (src/query.h:71)
+ENC_PLAIN, ENC_LZF, ENC_NUMBER, ENC_NULL = 0x00, 0x01, 0x02, 0xFF
+REPL_KVAL = 7
 
 
 class LzfLibraryMissing(ImportError):
@@ -69,6 +75,11 @@ def lib():
     L.lzf_host_decompress_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32]
     L.lzf_gpu_kernel_info.restype = ctypes.c_char_p
     L.lzf_gpu_kernel_info.argtypes = []
+    L.lzf_gpu_kv_frame_work_size.restype = u64
+    L.lzf_gpu_kv_frame_work_size.argtypes = [u32]
+    L.lzf_gpu_kv_frame.restype = ctypes.c_int
+    L.lzf_gpu_kv_frame.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, ctypes.c_int,
+                                   vp, u64, vp, vp, vp]
     del i32
     _LIB = L
     return L
@@ -162,3 +173,24 @@ def host_decompress_batch(inp, in_off, in_len, out, out_off, out_cap, out_len, e
                                          _np_ptr(out), _np_ptr(out_off), _np_ptr(out_cap),
                                          _np_ptr(out_len), _np_ptr(err), len(in_len))
     _check(rc, "lzf_host_decompress_batch")
+
+
+def kv_frame(keys, key_off, key_len, vals, val_off, val_size, enc, val_len, elements,
+             max_val_len, frame, max_response, frame_len, work=None, reply_header=True,
+             stream=None):
+    """MGET / KEYS reply (src/net.c:1256-1342, header src/net.c:1162-1205)
+    built on the device, LZF items decoded in place.  Tensors on one device:
+    keys/vals/enc/frame uint8, *_off int64, key_len/val_size/val_len int32,
+    frame_len int64 (1 element; 0 = CHECK_SPACE failed or an item did not
+    decode to its val_len).  ``work`` defaults to a fresh scratch tensor."""
+    import torch
+    n = key_len.numel()
+    if work is None:
+        work = torch.empty(int(lib().lzf_gpu_kv_frame_work_size(n)), dtype=torch.uint8,
+                           device=frame.device)
+    rc = lib().lzf_gpu_kv_frame(_ptr(keys), _ptr(key_off), _ptr(key_len), _ptr(vals),
+                                _ptr(val_off), _ptr(val_size), _ptr(enc), _ptr(val_len), n,
+                                int(elements), int(max_val_len), 1 if reply_header else 0,
+                                _ptr(frame), int(max_response), _ptr(frame_len), _ptr(work),
+                                _stream_handle(stream))
+    _check(rc, "lzf_gpu_kv_frame")

@@ -85,6 +85,43 @@ int lzf_host_decompress_batch(const uint8_t *in, const uint64_t *in_off, const u
                               uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
                               uint32_t *out_len, int32_t *err, uint32_t count);
 
+/*
+ * MGET / KEYS reply assembled on the device.
+ *
+ * Builds exactly the payload of gbClientEnqueueKeyValueSet
+ * (src/net.c:1256-1342) -- u32 `elements`, then per item that is not
+ * LZF_ENC_NULL: [u32 key size][key][u8 encoding][u32 value size][value],
+ * little-endian, LZF items emitted as PLAIN with their decoded bytes -- and,
+ * with reply_header != 0, the [i16 REPL_KVAL][u8 PLAIN][u32 size] reply
+ * header of gbClientEnqueueData (src/net.c:1162-1205) in front.
+ *
+ * Item i: key keys[key_off[i] .. +key_len[i]); encoding enc[i]; stored
+ * bytes vals[val_off[i] .. +val_size[i]) (the LZF stream for an LZF item,
+ * the 8-byte little-endian number for a NUMBER item, src/net.c:1321-1329).
+ * val_len[i] is the decoded length of an LZF item -- the original length
+ * recorded at SET time (the side table of §8(f) rank 3); max_val_len bounds
+ * it.  LZF items are decoded straight into the frame (no bounce buffer).
+ *
+ * frame must hold (reply_header ? 7 : 0) + max_response bytes.  On the
+ * device, *frame_len receives the frame's byte count, or 0 when the payload
+ * exceeds max_response (the reference's CHECK_SPACE, src/net.c:1272-1277)
+ * or an LZF item did not decode to val_len[i].  `work` is device scratch of
+ * lzf_gpu_kv_frame_work_size(count) bytes.
+ */
+#define LZF_ENC_PLAIN   0x00   /* GB_ENC_PLAIN,  src/net.h:274 */
+#define LZF_ENC_LZF     0x01   /* GB_ENC_LZF,    src/net.h:276 */
+#define LZF_ENC_NUMBER  0x02   /* GB_ENC_NUMBER, src/net.h:278 */
+#define LZF_ENC_NULL    0xFF   /* expired / missing item: skipped (src/net.c:1287) */
+#define LZF_REPL_KVAL   7      /* src/query.h:71 */
+
+uint64_t lzf_gpu_kv_frame_work_size(uint32_t count);
+int lzf_gpu_kv_frame(const uint8_t *keys, const uint64_t *key_off, const uint32_t *key_len,
+                     const uint8_t *vals, const uint64_t *val_off, const uint32_t *val_size,
+                     const uint8_t *enc, const uint32_t *val_len, uint32_t count,
+                     uint32_t elements, uint32_t max_val_len, int reply_header,
+                     uint8_t *frame, uint64_t max_response, uint64_t *frame_len, void *work,
+                     void *stream);
+
 /* Which kernel generation the batch calls dispatch to (diagnostics):
  * returns a static string such as "compress=window64 decompress=tokpar". */
 const char *lzf_gpu_kernel_info(void);

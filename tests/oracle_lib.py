@@ -62,6 +62,29 @@ class _Codec:
 class Oracle(_Codec):
     def __init__(self):
         super().__init__(ORACLE_SO, "oracle_lzf_compress", "oracle_lzf_decompress")
+        L = ctypes.CDLL(ORACLE_SO)
+        vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+        self.f = L.oracle_kv_frame
+        self.f.restype = ctypes.c_long
+        self.f.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, u32, u64, u32, ctypes.c_int, vp]
+
+    def kv_frame(self, items, elements, max_response, maxrequestsize, reply_header=True):
+        """items: [(key bytes, enc, stored bytes)]; the MGET reply frame
+        (src/net.c:1256-1342) or None where CHECK_SPACE fails."""
+        import numpy as np
+        keys = b"".join(k for k, _, _ in items) or b"\0"
+        vals = b"".join(v for _, _, v in items) or b"\0"
+        ko = np.cumsum([0] + [len(k) for k, _, _ in items[:-1]]).astype(np.uint64)
+        vo = np.cumsum([0] + [len(v) for _, _, v in items[:-1]]).astype(np.uint64)
+        kl = np.array([len(k) for k, _, _ in items], np.uint32)
+        vs = np.array([len(v) for _, _, v in items], np.uint32)
+        en = np.array([e for _, e, _ in items], np.uint8)
+        out = ctypes.create_string_buffer(max_response + 16)
+        kb, vb = ctypes.create_string_buffer(keys, len(keys)), ctypes.create_string_buffer(vals, len(vals))
+        P = lambda a: ctypes.c_void_p(a.ctypes.data)
+        r = self.f(kb, P(ko), P(kl), vb, P(vo), P(vs), P(en), len(items), elements,
+                   max_response, maxrequestsize, 1 if reply_header else 0, out)
+        return out.raw[:r] if r >= 0 else None
 
 
 def reference():
