@@ -383,39 +383,49 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
         const uint32_t sm = slot_mix(s);          /* bijective 16-bit mix of the slot */
         const uint32_t b = bucket_of(sm);
         const uint32_t k1 = ident_of(sm);
-        HeadT hv = H::EMPTY;
-        uint32_t hch = 0;                         /* chain entry of the bucket head */
-        if (valid) hv = L.head[b];
+        /* Lanes past lim_lane take part unconditionally (no exec-mask
+         * regions): their bits only ever land above every valid lane, where
+         * prevW (lanes below), `other` and `last` (masked by INS) never look,
+         * and their lookups are switched off below. */
+        const HeadT hv = L.head[b];
+        const uint32_t hch = L.chain[L.ci(H::empty(hv) ? 0u : H::pos(hv))];   /* head's chain entry */
         const uint32_t k2 = (sm >> (16 - CW_HBITS)) & (CW_T2 - 1u), k3 = sm >> 12;
         const unsigned long long me = 1ull << lane;
-        if (valid) {
-            atomicOr(&L.t1[k1], me);
-            atomicOr(&L.t2[k2], me);
-            atomicOr(&L.t3[k3], me);
-        }
+        atomicOr(&L.t1[k1], me);
+        atomicOr(&L.t2[k2], me);
+        atomicOr(&L.t3[k3], me);
         wave_lds_fence();
-        uint64_t M1 = 0, M2 = 0, M3 = 0;
-        if (valid) {
-            M1 = L.t1[k1];
-            M2 = L.t2[k2];
-            M3 = L.t3[k3];
-            if (!H::empty(hv)) hch = L.chain[L.ci(H::pos(hv))];
-        }
+        const uint64_t M1 = L.t1[k1], M2 = L.t2[k2], M3 = L.t3[k3];
         wave_lds_fence();
-        if (valid) {
-            L.t1[k1] = 0ull;
-            L.t2[k2] = 0ull;
-            L.t3[k3] = 0ull;
-        }
+        L.t1[k1] = 0ull;
+        L.t2[k2] = 0ull;
+        L.t3[k3] = 0ull;
         const uint64_t Mb = M2 & M3;              /* lanes with my bucket (mix bits 6-15) */
         const uint64_t Ms = M1 & Mb;              /* lanes with my slot (all 16 bits) */
         const uint64_t msb = Ms & lanemask_lt(lane);
         int prevW = msb ? (int)(63u - (uint32_t)__builtin_clzll(msb)) : -1;
         CW_PHASE(2);
 
-        /* ---- 2. exact table lookup among positions < P --------------- */
+        /* ---- 2. exact table lookup among positions < P (cw_lookup for
+         * the lanes without prevW, as one wave-uniform loop: every lane
+         * steps each round, the finished ones re-read their own entry) --- */
         uint32_t T = 0xFFFFFFFFu;
-        if (valid && prevW < 0) T = cw_lookup<HeadT, WRAP>(L, hv, hch, s, k1, p);
+        {
+            bool act = valid && prevW < 0 && (H::filter(hv) & filter_bit(k1)) &&
+                       p - H::pos(hv) <= LZF_WINDOW;
+            uint32_t q = act ? H::pos(hv) : 0u, d = hch;
+            if (act && H::ident(hv) == k1) T = q;
+            act = act && H::ident(hv) != k1;
+            while (__ballot(act)) {
+                act = act && d != 0u;                 /* skip q's run of its slot */
+                q = act ? q - d : q;
+                const uint32_t sq = slot_of(L.rd4(q) & 0xFFFFFFu);
+                d = L.chain[L.ci(q)];
+                act = act && p - q <= LZF_WINDOW;
+                if (act && sq == s) T = q;
+                act = act && sq != s;
+            }
+        }
         CW_PHASE(3);
 
         /* ---- 3. match test (src/lzf_c.c:151-166), probed length ------ */
