@@ -57,6 +57,9 @@
 #define CW_RING_MAX  16384u
 #define CW_EXT_CAP   19u          /* per-lane match length probe (3 + 4 x 4 bytes) */
 #define CW_TBYTES    (CW_TALL * 8u)
+#ifndef CW_ASM_WALK
+#define CW_ASM_WALK  1
+#endif
 
 /* Diagnostic build only (make stats -> liblzf_hip_stats.so): per-phase
  * s_memtime cycles and event counts, summed over all waves. */
@@ -468,22 +471,47 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
             const uint64_t first = MMc & ~lanemask_lt(j0);
             uint32_t j = first ? (uint32_t)__builtin_ctzll(first) : CW_LANES;
             exitLane = -1;
-            while (j < lim_lane) {
-                MMV |= 1ull << j;
-                if ((NXc >> j) & 1ull) {
-                    CW_STAT_ADD(coop, 1);
-                    const uint32_t mj = cw_coop_len(L, P + j, readlane_u32(ref, j),
-                                                    readlane_u32(m, j), readlane_u32(lim, j));
-                    if (lane == j) m = mj;
-                    NXc &= ~(1ull << j);
-                    if (j + mj >= lim_lane) { exitLane = (int)j; mexit = mj; break; }
-                    const uint64_t a = MMc & ~lanemask_lt(j + mj);
-                    j = a ? (uint32_t)__builtin_ctzll(a) : CW_LANES;
-                } else {
-                    const uint32_t nj = readlane_u32(nm, j);
-                    if (nj == 255u) { exitLane = (int)j; mexit = readlane_u32(m, j); break; }
-                    j = nj;
+            uint32_t jl = 0;                      /* the last orbit match lane so far */
+            for (;;) {
+                /* the common steps: match lanes of exact length follow nm */
+#if CW_ASM_WALK
+                /* seven scalar instructions per orbit match (s_bitcmp1 /
+                 * s_bitset1 / v_readlane; the nop covers the readlane's
+                 * lane-select hazard on the next step) */
+                asm volatile(
+                    "L%=_top:\n\t"
+                    "s_cmp_lt_u32 %0, %4\n\t"
+                    "s_cbranch_scc0 L%=_end\n\t"
+                    "s_bitcmp1_b64 %3, %0\n\t"
+                    "s_cbranch_scc1 L%=_end\n\t"
+                    "s_bitset1_b64 %2, %0\n\t"
+                    "s_mov_b32 %1, %0\n\t"
+                    "v_readlane_b32 %0, %5, %0\n\t"
+                    "s_nop 4\n\t"
+                    "s_branch L%=_top\n"
+                    "L%=_end:"
+                    : "+s"(j), "+s"(jl), "+s"(MMV)
+                    : "s"(NXc), "s"(lim_lane), "v"(nm)
+                    : "scc");
+#else
+                while (j < lim_lane && !((NXc >> j) & 1ull)) {
+                    MMV |= 1ull << j;
+                    jl = j;
+                    j = readlane_u32(nm, j);
                 }
+#endif
+                if (j == 255u) { exitLane = (int)jl; mexit = readlane_u32(m, jl); break; }
+                if (j >= lim_lane) break;
+                /* a match that reached the probe cap: exact length by the whole wave */
+                CW_STAT_ADD(coop, 1);
+                MMV |= 1ull << j;
+                const uint32_t mj = cw_coop_len(L, P + j, readlane_u32(ref, j),
+                                                readlane_u32(m, j), readlane_u32(lim, j));
+                if (lane == j) m = mj;
+                NXc &= ~(1ull << j);
+                if (j + mj >= lim_lane) { exitLane = (int)j; mexit = mj; break; }
+                const uint64_t a = MMc & ~lanemask_lt(j + mj);
+                j = a ? (uint32_t)__builtin_ctzll(a) : CW_LANES;
             }
             end = exitLane >= 0 ? (uint32_t)exitLane + 1u : lim_lane;
             /* visited = not strictly inside the reach of an earlier orbit match */
@@ -551,20 +579,24 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
          * previous (address, byte).  Literal: [rollover header 31 at pos-32]
          * + the byte.  Match: [run header] + 2 or 3 back-reference bytes.
          * Out of space (src/lzf_c.c:176, 263): nothing of the lane is stored. */
+        const uint32_t lit = L.rd1(p);
+        asm volatile("" ::"v"(lit));              /* load for every lane: no branch around it */
         const uint32_t off = p - ref - 1u;
         const uint32_t Lc = m - 2u;
         const uint32_t pos = myH0 + (isM ? Tr : nf);
-        const bool lfail = visited && (isM ? pos + 4u >= cap : pos >= cap);
-        const uint32_t b0 = isM ? ((off >> 8) | (Lc < 7u ? Lc << 5 : 0xE0u)) : L.rd1(p);
+        const bool lfail = visited & (pos + (isM ? 4u : 0u) >= cap);
+        const uint32_t b0 = isM ? ((off >> 8) | (Lc < 7u ? Lc << 5 : 0xE0u)) : lit;
         const bool h1 = isM ? (R & 31u) != 0u : (R & 31u) == 31u;
-        const uint32_t a1 = h1 ? (isM ? myH0 + 33u * (R >> 5) : pos - 32u) : pos;
+        const uint32_t hpos = myH0 + 33u * (R >> 5);              /* the run's header */
+        asm volatile("" ::"v"(hpos));
+        const uint32_t a1 = h1 ? (isM ? hpos : pos - 32u) : pos;
         const uint32_t v1 = h1 ? (isM ? (R & 31u) - 1u : 31u) : b0;
         const uint32_t a3 = isM ? pos + 1u : pos;
         const uint32_t v3 = isM ? (Lc < 7u ? off : Lc - 7u) : b0;
-        const bool long3 = isM && Lc >= 7u;
+        const bool long3 = isM & (Lc >= 7u);
         const uint32_t a4 = long3 ? pos + 2u : a3;
         const uint32_t v4 = long3 ? off : v3;
-        if (visited && !lfail) {
+        if (visited & !lfail) {
             dst[a1] = (uint8_t)v1;
             dst[pos] = (uint8_t)b0;
             dst[a3] = (uint8_t)v3;
@@ -598,20 +630,24 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
         }
 
         /* ---- 6. insert the window's inserted positions --------------- */
-        if ((INS >> lane) & 1ull) {
+        {
+            /* skip target of every lane, branch-free: the latest earlier
+             * inserted window lane of the bucket with another slot, else the
+             * bucket head (or the head's own target when it has my slot) */
+            const bool ins = (INS >> lane) & 1ull;
             const bool last = (Mb & INS & ~lanemask_lt(lane + 1u)) == 0ull;
             const uint64_t other = Mb & ~Ms & INS & lanemask_lt(lane);
-            uint32_t y = 0xFFFFFFFFu;
-            if (other) {
-                y = P + 63u - (uint32_t)__builtin_clzll(other);
-            } else if (!H::empty(hv) && p - H::pos(hv) <= LZF_WINDOW) {
-                const uint32_t hp = H::pos(hv);
-                if (H::ident(hv) != k1) y = hp;
-                else if (hch) y = hp - hch;
+            const uint32_t hp = H::pos(hv);
+            const bool hok = !H::empty(hv) & (p - hp <= LZF_WINDOW);
+            const uint32_t yh = H::ident(hv) != k1 ? hp : (hch ? hp - hch : 0xFFFFFFFFu);
+            const uint32_t y = other ? P + 63u - (uint32_t)__builtin_clzll(other)
+                                     : (hok ? yh : 0xFFFFFFFFu);
+            const uint32_t cv = (y != 0xFFFFFFFFu && p - y <= LZF_WINDOW) ? p - y : 0u;
+            if (ins) {
+                L.chain[L.ci(p)] = (uint16_t)cv;
+                head_mark(L.head, b, k1);
+                if (last) head_set(L.head, b, k1, p);
             }
-            L.chain[L.ci(p)] = (uint16_t)((y != 0xFFFFFFFFu && p - y <= LZF_WINDOW) ? p - y : 0u);
-            head_mark(L.head, b, k1);
-            if (last) head_set(L.head, b, k1, p);
         }
         wave_lds_fence();
         if (tx0 != 0xFFFFFFFFu || tx1 != 0xFFFFFFFFu) {
