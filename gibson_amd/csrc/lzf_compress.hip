@@ -22,7 +22,7 @@
  *      where the reference's `off < MAX_OFF` test fails too;
  *   3. match test and length per lane (src/lzf_c.c:151-209, including the 16
  *      unconditional compares: lim = maxlen>16 ? max(maxlen,19) : maxlen),
- *      probed up to 11 bytes per lane;
+ *      probed up to 19 bytes per lane;
  *   4. the parse orbit: a minimal scalar loop over match lanes (s_ff1 on the
  *      ballot); a match on the orbit that reached the probe cap gets its
  *      exact length from a whole-wave 256-byte compare.  A visited lane
@@ -432,18 +432,18 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
         CW_PHASE(3);
 
         /* ---- 3. match test (src/lzf_c.c:151-166), probed length ------ */
+        /* (every lane runs the test and the probe: no exec-mask regions;
+         * a lane without a candidate reads its own position) */
         uint32_t ref = prevW >= 0 ? P + (uint32_t)prevW : T;
-        const bool match = valid && ref != 0xFFFFFFFFu && ref > 0u &&
-                           (p - ref - 1u) < LZF_WINDOW && p + 4u < n &&
-                           (L.rd4(ref) & 0xFFFFFFu) == tri;
-        uint32_t lim = 0, m = 1;
-        bool exact = true;
-        if (match) {
-            lim = match_lim(n, p);
-            const uint32_t kc = lim < CW_EXT_CAP ? lim : CW_EXT_CAP;
-            m = cw_probe(L, p, ref, kc);        /* bytes [3, kc) in one go */
-            exact = (m < kc) || (kc == lim);
-        }
+        const bool cand = valid & (ref != 0xFFFFFFFFu) & (ref > 0u) &
+                          ((p - ref - 1u) < LZF_WINDOW) & (p + 4u < n);
+        const uint32_t rr = cand ? ref : p;
+        const bool match = cand & ((L.rd4(rr) & 0xFFFFFFu) == tri);
+        const uint32_t lim0 = match_lim(n, p);
+        const uint32_t kc = lim0 < CW_EXT_CAP ? lim0 : CW_EXT_CAP;
+        const uint32_t mp = cw_probe(L, p, rr, kc);  /* bytes [3, kc) in one go */
+        uint32_t lim = match ? lim0 : 0u, m = match ? mp : 1u;
+        const bool exact = !match | (mp < kc) | (kc == lim0);
         CW_PHASE(4);
 
         /* ---- 4. the parse orbit -----------------------------------------
