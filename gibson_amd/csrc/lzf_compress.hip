@@ -57,6 +57,9 @@
 #define CW_RING_MAX  16384u
 #define CW_EXT_CAP   19u          /* per-lane match length probe (3 + 4 x 4 bytes) */
 #define CW_TBYTES    (CW_TALL * 8u)
+#ifndef CW_HOPCAP
+#define CW_HOPCAP    3u           /* chain hops in the wave-uniform lookup loop */
+#endif
 #ifndef CW_ASM_WALK
 #define CW_ASM_WALK  1
 #endif
@@ -295,6 +298,22 @@ __device__ __forceinline__ uint32_t cd_incl_max(uint32_t x)
     return x;
 }
 
+/* One wave-uniform round of the table walk (cw_lookup) for every lane still
+ * active: skip q's run of its slot, check the next entry.  Finished lanes
+ * re-read their own entry. */
+template <typename HeadT, bool WRAP>
+__device__ __forceinline__ void cw_walk_step(const CwLds<HeadT, WRAP> &L, uint32_t p, uint32_t s, bool &act,
+                                             uint32_t &q, uint32_t &d, uint32_t &T)
+{
+    act = act && d != 0u;
+    q = act ? q - d : q;
+    const uint32_t sq = slot_of(L.rd4(q) & 0xFFFFFFu);
+    d = L.chain[L.ci(q)];
+    act = act && p - q <= LZF_WINDOW;
+    if (act && sq == s) T = q;
+    act = act && sq != s;
+}
+
 __device__ __forceinline__ uint32_t match_lim(uint32_t n, uint32_t p)
 {
     uint32_t maxlen = n - p - 2u;
@@ -413,37 +432,37 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
          * the lanes without prevW, as one wave-uniform loop: every lane
          * steps each round, the finished ones re-read their own entry) --- */
         uint32_t T = 0xFFFFFFFFu;
-        {
-            bool act = valid && prevW < 0 && (H::filter(hv) & filter_bit(k1)) &&
-                       p - H::pos(hv) <= LZF_WINDOW;
-            uint32_t q = act ? H::pos(hv) : 0u, d = hch;
-            if (act && H::ident(hv) == k1) T = q;
-            act = act && H::ident(hv) != k1;
-            while (__ballot(act)) {
-                act = act && d != 0u;                 /* skip q's run of its slot */
-                q = act ? q - d : q;
-                const uint32_t sq = slot_of(L.rd4(q) & 0xFFFFFFu);
-                d = L.chain[L.ci(q)];
-                act = act && p - q <= LZF_WINDOW;
-                if (act && sq == s) T = q;
-                act = act && sq != s;
-            }
-        }
+        bool act = valid && prevW < 0 && (H::filter(hv) & filter_bit(k1)) && p - H::pos(hv) <= LZF_WINDOW;
+        uint32_t wq = act ? H::pos(hv) : 0u, wd = hch;           /* walk state */
+        if (act && H::ident(hv) == k1) T = wq;
+        act = act && H::ident(hv) != k1;
+        /* walks are cut off at CW_HOPCAP hops (unrolled: no loop branch);
+         * their lanes count as literals for now and are finished (all at
+         * once) only if the orbit visits one of them */
+#pragma unroll
+        for (uint32_t it = 0; it < CW_HOPCAP; it++) cw_walk_step(L, p, s, act, wq, wd, T);
+        uint64_t U = __ballot(act);
         CW_PHASE(3);
 
         /* ---- 3. match test (src/lzf_c.c:151-166), probed length ------ */
         /* (every lane runs the test and the probe: no exec-mask regions;
          * a lane without a candidate reads its own position) */
         uint32_t ref = prevW >= 0 ? P + (uint32_t)prevW : T;
-        const bool cand = valid & (ref != 0xFFFFFFFFu) & (ref > 0u) &
-                          ((p - ref - 1u) < LZF_WINDOW) & (p + 4u < n);
-        const uint32_t rr = cand ? ref : p;
-        const bool match = cand & ((L.rd4(rr) & 0xFFFFFFu) == tri);
         const uint32_t lim0 = match_lim(n, p);
         const uint32_t kc = lim0 < CW_EXT_CAP ? lim0 : CW_EXT_CAP;
-        const uint32_t mp = cw_probe(L, p, rr, kc);  /* bytes [3, kc) in one go */
-        uint32_t lim = match ? lim0 : 0u, m = match ? mp : 1u;
-        const bool exact = !match | (mp < kc) | (kc == lim0);
+        bool match, exact;
+        uint32_t lim, m;
+        auto match_test = [&]() {
+            const bool cand = valid & (ref != 0xFFFFFFFFu) & (ref > 0u) &
+                              ((p - ref - 1u) < LZF_WINDOW) & (p + 4u < n);
+            const uint32_t rr = cand ? ref : p;
+            match = cand & ((L.rd4(rr) & 0xFFFFFFu) == tri);
+            const uint32_t mp = cw_probe(L, p, rr, kc);   /* bytes [3, kc) in one go */
+            lim = match ? lim0 : 0u;
+            m = match ? mp : 1u;
+            exact = !match | (mp < kc) | (kc == lim0);
+        };
+        match_test();
         CW_PHASE(4);
 
         /* ---- 4. the parse orbit -----------------------------------------
@@ -523,9 +542,41 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
             const uint64_t INTR = ~V & ~(V >> 1) & ~(V >> 2);    /* inside a match */
             const bool vis = (V >> lane) & 1ull;
             const uint64_t BADC = __ballot(vis && prevW >= 0 && ((INTR >> (uint32_t)prevW) & 1ull));
-            if (!BADC) break;
-            /* lane f read an entry the reference never inserted: its ref is
-             * the latest INSERTED same-slot lane, else the table entry */
+            const uint64_t BADU = U & V;
+            if (!(BADC | BADU)) break;
+            if (BADU && (!BADC || __builtin_ctzll(BADU) < __builtin_ctzll(BADC))) {
+                /* a visited lane's table walk was cut off: finish every cut-off
+                 * walk (one wave-uniform loop); if some of them now match,
+                 * redo their match tests and, when one of those is visited,
+                 * walk the orbit again from it */
+                CW_STAT_ADD(hops, 1);
+                const bool was = (U >> lane) & 1ull;
+                while (__ballot(act)) cw_walk_step(L, p, s, act, wq, wd, T);
+                const bool cu = was & (T != 0xFFFFFFFFu) & (T > 0u) & ((p - T - 1u) < LZF_WINDOW) &
+                                (p + 4u < n) & ((L.rd4(was && T != 0xFFFFFFFFu ? T : p) & 0xFFFFFFu) == tri);
+                const uint64_t newM = __ballot(cu);
+                if (newM) {
+                    const bool om = match, oe = exact;
+                    const uint32_t oref = ref, olim = lim, omm = m;
+                    if (was) ref = T;
+                    match_test();
+                    if (!was) { match = om; exact = oe; ref = oref; lim = olim; m = omm; }
+                    MMc |= newM;
+                    NXc |= __ballot(!exact) & newM;
+                }
+                U = 0;
+                const uint64_t chg = newM & V;
+                if (chg) {
+                    const uint32_t f = (uint32_t)__builtin_ctzll(chg);
+                    MMV &= lanemask_lt(f);
+                    j0 = f;
+                    continue;
+                }
+                if (!BADC) break;
+            }
+            /* lane f read an entry the reference never inserted (or its table
+             * walk was cut off): its ref is the latest INSERTED same-slot lane,
+             * else the table entry */
             CW_STAT_ADD(trunc, 1);
             const uint32_t f = (uint32_t)__builtin_ctzll(BADC);
             const uint64_t alt = readlane_u64(Ms, f) & lanemask_lt(f) & ~INTR;
