@@ -496,9 +496,34 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
 #if CW_ASM_WALK
                 /* seven scalar instructions per orbit match (s_bitcmp1 /
                  * s_bitset1 / v_readlane; the nop covers the readlane's
-                 * lane-select hazard on the next step) */
+                 * lane-select hazard on the next step), unrolled 4x so the
+                 * loop takes one backward branch per four matches */
                 asm volatile(
                     "L%=_top:\n\t"
+                    "s_cmp_lt_u32 %0, %4\n\t"
+                    "s_cbranch_scc0 L%=_end\n\t"
+                    "s_bitcmp1_b64 %3, %0\n\t"
+                    "s_cbranch_scc1 L%=_end\n\t"
+                    "s_bitset1_b64 %2, %0\n\t"
+                    "s_mov_b32 %1, %0\n\t"
+                    "v_readlane_b32 %0, %5, %0\n\t"
+                    "s_nop 4\n\t"
+                    "s_cmp_lt_u32 %0, %4\n\t"
+                    "s_cbranch_scc0 L%=_end\n\t"
+                    "s_bitcmp1_b64 %3, %0\n\t"
+                    "s_cbranch_scc1 L%=_end\n\t"
+                    "s_bitset1_b64 %2, %0\n\t"
+                    "s_mov_b32 %1, %0\n\t"
+                    "v_readlane_b32 %0, %5, %0\n\t"
+                    "s_nop 4\n\t"
+                    "s_cmp_lt_u32 %0, %4\n\t"
+                    "s_cbranch_scc0 L%=_end\n\t"
+                    "s_bitcmp1_b64 %3, %0\n\t"
+                    "s_cbranch_scc1 L%=_end\n\t"
+                    "s_bitset1_b64 %2, %0\n\t"
+                    "s_mov_b32 %1, %0\n\t"
+                    "v_readlane_b32 %0, %5, %0\n\t"
+                    "s_nop 4\n\t"
                     "s_cmp_lt_u32 %0, %4\n\t"
                     "s_cbranch_scc0 L%=_end\n\t"
                     "s_bitcmp1_b64 %3, %0\n\t"
