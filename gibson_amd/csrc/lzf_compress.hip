@@ -385,7 +385,7 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
          * ring also still holds the 8 KiB back-reference span */
         uint32_t need = P + CW_LANES + LZF_MAX_REF + 16u;
         if (need > n) need = n;
-        if (loaded < need) {
+        if (__builtin_expect(loaded < need, 0)) {
             uint32_t to = loaded + 4096u;
             if (to < need) to = (need + 15u) & ~15u;
             if (to > n) to = n;
@@ -544,8 +544,8 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
                     j = readlane_u32(nm, j);
                 }
 #endif
-                if (j == 255u) { exitLane = (int)jl; mexit = readlane_u32(m, jl); break; }
-                if (j >= lim_lane) break;
+                if (__builtin_expect(j == 255u, 1)) { exitLane = (int)jl; mexit = readlane_u32(m, jl); break; }
+                if (__builtin_expect(j >= lim_lane, 1)) break;
                 /* a match that reached the probe cap: exact length by the whole wave */
                 CW_STAT_ADD(coop, 1);
                 MMV |= 1ull << j;
@@ -568,7 +568,7 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
             const bool vis = (V >> lane) & 1ull;
             const uint64_t BADC = __ballot(vis && prevW >= 0 && ((INTR >> (uint32_t)prevW) & 1ull));
             const uint64_t BADU = U & V;
-            if (!(BADC | BADU)) break;
+            if (__builtin_expect(!(BADC | BADU), 1)) break;
             if (BADU && (!BADC || __builtin_ctzll(BADU) < __builtin_ctzll(BADC))) {
                 /* a visited lane's table walk was cut off: finish every cut-off
                  * walk (one wave-uniform loop); if some of them now match,
@@ -678,7 +678,7 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
             dst[a3] = (uint8_t)v3;
             dst[a4] = (uint8_t)v4;
         }
-        if (__ballot(lfail)) { fail = true; break; }
+        if (__builtin_expect(__ballot(lfail) != 0, 0)) { fail = true; break; }
         CW_PHASE(6);
 
         /* ---- carry the cursor state to the next window ---------------- */
