@@ -60,9 +60,6 @@
 #ifndef CW_HOPCAP
 #define CW_HOPCAP    3u           /* chain hops in the wave-uniform lookup loop */
 #endif
-#ifndef CW_ASM_WALK
-#define CW_ASM_WALK  1
-#endif
 
 /* Diagnostic build only (make stats -> liblzf_hip_stats.so): per-phase
  * s_memtime cycles and event counts, summed over all waves. */
@@ -493,7 +490,6 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
             uint32_t jl = 0;                      /* the last orbit match lane so far */
             for (;;) {
                 /* the common steps: match lanes of exact length follow nm */
-#if CW_ASM_WALK
                 /* seven scalar instructions per orbit match (s_bitcmp1 /
                  * s_bitset1 / v_readlane; the nop covers the readlane's
                  * lane-select hazard on the next step), unrolled 4x so the
@@ -537,26 +533,23 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
                     : "+s"(j), "+s"(jl), "+s"(MMV)
                     : "s"(NXc), "s"(lim_lane), "v"(nm)
                     : "scc");
-#else
-                while (j < lim_lane && !((NXc >> j) & 1ull)) {
-                    MMV |= 1ull << j;
-                    jl = j;
-                    j = readlane_u32(nm, j);
-                }
-#endif
-                if (__builtin_expect(j == 255u, 1)) { exitLane = (int)jl; mexit = readlane_u32(m, jl); break; }
+                /* the walk stopped: past the window (j == 255 after a match
+                 * that leaves it, CW_LANES after a literal) -- or at a match
+                 * that reached the probe cap, whose exact length the whole
+                 * wave computes; then it goes on (one exit, no flow flags) */
                 if (__builtin_expect(j >= lim_lane, 1)) break;
-                /* a match that reached the probe cap: exact length by the whole wave */
                 CW_STAT_ADD(coop, 1);
                 MMV |= 1ull << j;
+                jl = j;
                 const uint32_t mj = cw_coop_len(L, P + j, readlane_u32(ref, j),
                                                 readlane_u32(m, j), readlane_u32(lim, j));
                 if (lane == j) m = mj;
                 NXc &= ~(1ull << j);
-                if (j + mj >= lim_lane) { exitLane = (int)j; mexit = mj; break; }
-                const uint64_t a = MMc & ~lanemask_lt(j + mj);
-                j = a ? (uint32_t)__builtin_ctzll(a) : CW_LANES;
+                const uint64_t a = j + mj >= lim_lane ? 0ull : MMc & ~lanemask_lt(j + mj);
+                j = j + mj >= lim_lane ? 255u : (a ? (uint32_t)__builtin_ctzll(a) : CW_LANES);
             }
+            exitLane = j == 255u ? (int)jl : -1;
+            mexit = readlane_u32(m, jl);
             end = exitLane >= 0 ? (uint32_t)exitLane + 1u : lim_lane;
             /* visited = not strictly inside the reach of an earlier orbit match */
             /* (orbit match lanes are visited; their own reach is > lane) */
