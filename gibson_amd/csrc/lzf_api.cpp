@@ -31,14 +31,19 @@ hipError_t lzf_launch_decompress_serial(const LzfBatch &b, hipStream_t s);
 
 namespace {
 
-enum KernelGen { GEN_PARALLEL = 0, GEN_SERIAL = 1 };
+enum KernelGen { GEN_LANE = 0, GEN_WINDOW = 1, GEN_SERIAL = 2 };
 
-/* LZF_GPU_KERNEL=serial selects the single-lane generation (diagnostics,
- * cross-checks); read per launch so one process can A/B both. */
+/* LZF_GPU_KERNEL picks the kernel generation, read per launch so one process
+ * can A/B them: "lane" (default; one lane per value, lzf_lane.hip),
+ * "window" (one wave per value: window64 / tokpar64) or "serial" (the
+ * single-lane first generation).  All are bit-exact; the GPU tests
+ * cross-check them. */
 KernelGen kernel_gen()
 {
     const char *e = getenv("LZF_GPU_KERNEL");
-    return (e && !strcmp(e, "serial")) ? GEN_SERIAL : GEN_PARALLEL;
+    if (e && !strcmp(e, "serial")) return GEN_SERIAL;
+    if (e && !strcmp(e, "window")) return GEN_WINDOW;
+    return GEN_LANE;
 }
 
 bool device_ok(int dev)
@@ -62,18 +67,79 @@ int current_device_ok()
     return device_ok(dev) ? LZF_GPU_OK : LZF_GPU_ENODEV;
 }
 
+/* Compress scratch of the lane generation (cand words + inserted bitmap),
+ * one per (host thread, device), grown on demand up to LZF_GPU_SCRATCH_MB
+ * (default 12 GiB; larger batches run in chunks).  A batch on another stream
+ * than the previous user waits for that user's kernels first. */
+struct Scratch {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    hipStream_t last = nullptr;
+    bool used = false;
+};
+
+size_t scratch_limit()
+{
+    const char *e = getenv("LZF_GPU_SCRATCH_MB");
+    unsigned long long mb = e ? strtoull(e, nullptr, 10) : 12288ull;
+    if (mb < 1) mb = 1;
+    return (size_t)mb << 20;
+}
+
+hipError_t lane_compress(const LzfBatch &b, hipStream_t s)
+{
+    static thread_local Scratch per_dev[64];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    Scratch &S = per_dev[dev & 63];
+    const size_t per = lzf_lane_scratch_per_value(b.max_len);
+    size_t want = per * (size_t)b.count + 512;
+    const size_t lim = scratch_limit();
+    if (want > lim) want = lim;
+    if (want < per + 512) want = per + 512;
+    if (S.cap < want) {
+        if (S.p) {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(S.p);
+            S.p = nullptr;
+            S.cap = 0;
+        }
+        e = hipMalloc(&S.p, want);
+        if (e != hipSuccess) return e;
+        S.cap = want;
+        S.used = false;
+    }
+    if (!S.ev && (e = hipEventCreateWithFlags(&S.ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if (S.used && S.last != s && (e = hipStreamWaitEvent(s, S.ev, 0)) != hipSuccess) return e;
+    const char *ff = getenv("LZF_GPU_LANE_FORCE_FIX");
+    e = lzf_launch_compress_lane(b, s, S.p, S.cap, (ff && *ff == '1') ? 1u : 0u);
+    if (e != hipSuccess) return e;
+    e = hipEventRecord(S.ev, s);
+    S.last = s;
+    S.used = true;
+    return e;
+}
+
 hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
 {
-    if (kernel_gen() == GEN_SERIAL || !lzf_compress_kernel_name())
-        return lzf_launch_compress_serial(b, s);
-    return lzf_launch_compress(b, s);
+    switch (kernel_gen()) {
+    case GEN_SERIAL: return lzf_launch_compress_serial(b, s);
+    case GEN_WINDOW: return lzf_launch_compress(b, s);
+    default:
+        /* values past 64 KiB go to the window generation (64-bit heads) */
+        return lzf_lane_compress_supported(b.max_len) ? lane_compress(b, s) : lzf_launch_compress(b, s);
+    }
 }
 
 hipError_t launch_decompress(const LzfBatch &b, hipStream_t s)
 {
-    if (kernel_gen() == GEN_SERIAL || !lzf_decompress_kernel_name())
-        return lzf_launch_decompress_serial(b, s);
-    return lzf_launch_decompress(b, s);
+    switch (kernel_gen()) {
+    case GEN_SERIAL: return lzf_launch_decompress_serial(b, s);
+    case GEN_WINDOW: return lzf_launch_decompress(b, s);
+    default: return lzf_launch_decompress_lane(b, s);
+    }
 }
 
 [[noreturn]] void die(const char *what, hipError_t e)
@@ -345,11 +411,14 @@ int lzf_gpu_kv_frame(const uint8_t *keys, const uint64_t *key_off, const uint32_
 const char *lzf_gpu_kernel_info(void)
 {
     static thread_local std::string s;
-    bool ser = kernel_gen() == GEN_SERIAL;
-    const char *c = lzf_compress_kernel_name();
-    const char *d = lzf_decompress_kernel_name();
-    s = std::string("compress=") + ((ser || !c) ? "serial" : c) +
-        " decompress=" + ((ser || !d) ? "serial" : d);
+    switch (kernel_gen()) {
+    case GEN_SERIAL: s = "compress=serial decompress=serial"; break;
+    case GEN_WINDOW:
+        s = std::string("compress=") + lzf_compress_kernel_name() + " decompress=" +
+            lzf_decompress_kernel_name();
+        break;
+    default: s = "compress=lane(cand+parse; window64 past 64 KiB) decompress=lane"; break;
+    }
     return s.c_str();
 }
 

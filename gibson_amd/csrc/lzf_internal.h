@@ -53,7 +53,22 @@ struct LzfFrameArgs {
     uint8_t *w_skip;
 };
 
+/* compress scratch of the lane generation (lzf_lane.hip), device pointers:
+ * per value cstride u16 cand words and bstride u32 inserted-bitmap words */
+struct LzfLaneScratch {
+    uint16_t *cand;
+    uint32_t *bits;
+    uint64_t cstride;
+    uint64_t bstride;
+    uint32_t force_fix;    /* diagnostics: take the atomic-order repair path */
+};
+
 /* launchers, defined next to their kernels; return hipSuccess or the error */
+hipError_t lzf_launch_decompress_lane(const LzfBatch &b, hipStream_t s);
+hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scratch,
+                                    size_t scratch_bytes, uint32_t force_fix);
+size_t lzf_lane_scratch_per_value(uint32_t max_len);
+bool lzf_lane_compress_supported(uint32_t max_len);
 hipError_t lzf_launch_compress(const LzfBatch &b, hipStream_t s);
 hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s);
 hipError_t lzf_launch_synth(int kind, uint64_t seed, uint64_t first, uint64_t stride,

@@ -1,0 +1,758 @@
+/*
+ * lzf_lane.hip -- the "lane" generation of the LZF kernels for gfx950.
+ *
+ * Values are independent; the reference's loops over one value are serial
+ * (the token decoder src/lzf_d.c:64-146, the greedy parse src/lzf_c.c:145-274).
+ * This generation runs ONE LANE PER VALUE for the serial parts, so a wave
+ * advances 64 values at once and one VALU instruction does the work of 64
+ * scalar steps, instead of spending a whole wave on one value:
+ *
+ *   decompress  lzf_decompress_lane_kernel: one lane decodes one stream with
+ *               the reference's checks in the reference's order; literal runs
+ *               and back-references move as unaligned 16-byte pieces.
+ *
+ *   compress    two kernels per batch (chunked by the scratch size):
+ *     1. lzf_cand_*_kernel (one wave per value, position-parallel): for every
+ *        position p the nearest earlier position q with the same 16-bit slot
+ *        (src/lzf_c.c:47-57, HLOG 16) -- whether or not the parse will insert
+ *        q -- and how far the bytes at p and q agree (<= 8).  Packed into a
+ *        u16 per position in HBM scratch ("cand").  Bucket heads in LDS are
+ *        updated with ds_max_rtn in lane order, which hands every lane its
+ *        bucket predecessor; a per-position chain resolves bucket collisions.
+ *     2. lzf_parse_lane_kernel (one lane per value): the reference's greedy
+ *        parse and emission, bit-exact.  The reference's ref at p is the
+ *        latest INSERTED position of p's slot (src/lzf_c.c:147-149); every
+ *        position the parse visits is inserted, plus the last two positions
+ *        of each match (src/lzf_c.c:227-247), so ref(p) is the first
+ *        position on the cand chain from p that is not inside an earlier
+ *        match.  The lane keeps an inserted-bitmap of its value (HBM
+ *        scratch, the last five words in registers) and walks the chain only
+ *        past skipped positions.
+ *
+ * Scratch per value: 2 B/position (cand) + 1 bit/position (bitmap).
+ */
+#include "lzf_internal.h"
+
+/* ---- small helpers ------------------------------------------------------ */
+
+__device__ __forceinline__ uint4 ln_ld16(const uint8_t *p)          /* unaligned */
+{
+    uint4 v;
+    __builtin_memcpy(&v, p, 16);
+    return v;
+}
+
+__device__ __forceinline__ uint2 ln_ld8(const uint8_t *p)
+{
+    uint2 v;
+    __builtin_memcpy(&v, p, 8);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t ln_ld4(const uint8_t *p)
+{
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+}
+
+/* bytes [p, p + avail), avail < 16, zero beyond: never touches p + avail */
+__device__ __forceinline__ uint4 ln_ld16_tail(const uint8_t *p, uint32_t avail)
+{
+    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16u; k++) {
+        const uint32_t b = k < avail ? (uint32_t)p[k] : 0u;
+        const uint32_t s = 8u * (k & 3u);
+        if (k < 4u) w0 |= b << s;
+        else if (k < 8u) w1 |= b << s;
+        else if (k < 12u) w2 |= b << s;
+        else w3 |= b << s;
+    }
+    return make_uint4(w0, w1, w2, w3);
+}
+
+__device__ __forceinline__ uint4 ln_ld16_safe(const uint8_t *p, uint32_t avail)
+{
+    return avail >= 16u ? ln_ld16(p) : ln_ld16_tail(p, avail);
+}
+
+/* store exactly len (<= 16) bytes of v at p (unaligned) */
+__device__ __forceinline__ void ln_st_exact(uint8_t *p, uint4 v, uint32_t len)
+{
+    if (len >= 16u) {
+        __builtin_memcpy(p, &v, 16);
+        return;
+    }
+    uint32_t a = v.x, b = v.y, c = v.z, d = v.w;
+    if (len & 8u) {
+        uint2 t = make_uint2(a, b);
+        __builtin_memcpy(p, &t, 8);
+        p += 8;
+        a = c;
+        b = d;
+    }
+    if (len & 4u) {
+        __builtin_memcpy(p, &a, 4);
+        p += 4;
+        a = b;
+    }
+    if (len & 2u) {
+        const uint16_t t = (uint16_t)a;
+        __builtin_memcpy(p, &t, 2);
+        p += 2;
+        a >>= 16;
+    }
+    if (len & 1u) *p = (uint8_t)a;
+}
+
+__device__ __forceinline__ uint32_t ln_ab(uint32_t hi, uint32_t lo)    /* (hi:lo) >> 8 */
+{
+    return __builtin_amdgcn_alignbyte(hi, lo, 1u);
+}
+
+__device__ __forceinline__ uint32_t ln_sel4(uint4 v, uint32_t i)
+{
+    return i == 0u ? v.x : i == 1u ? v.y : i == 2u ? v.z : v.w;
+}
+
+__device__ __forceinline__ uint32_t ln_first_diff(uint4 a, uint4 b)   /* 16 if equal */
+{
+    uint32_t x;
+    if ((x = a.x ^ b.x)) return (uint32_t)__builtin_ctz(x) >> 3;
+    if ((x = a.y ^ b.y)) return 4u + ((uint32_t)__builtin_ctz(x) >> 3);
+    if ((x = a.z ^ b.z)) return 8u + ((uint32_t)__builtin_ctz(x) >> 3);
+    if ((x = a.w ^ b.w)) return 12u + ((uint32_t)__builtin_ctz(x) >> 3);
+    return 16u;
+}
+
+__device__ __forceinline__ void ln_wave_fence()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+/* slot(p) of src/lzf_c.c:47-57 (VERY_FAST, HLOG 16) from b[p..p+2] */
+__device__ __forceinline__ uint32_t ln_slot(uint32_t tri)
+{
+    const uint32_t b0 = tri & 0xFFu, b1 = (tri >> 8) & 0xFFu, b2 = (tri >> 16) & 0xFFu;
+    return (((b0 << 8) | b1) - 5u * ((b1 << 8) | b2)) & 0xFFFFu;
+}
+
+/* bijective 16-bit mix of the slot: bucket = high bits, identity = low bits */
+__device__ __forceinline__ uint32_t ln_mix(uint32_t s) { return (s * 40503u) & 0xFFFFu; }
+
+/* ======================================================================== */
+/* decompress: one lane per stream                                          */
+/* ======================================================================== */
+
+#define LD_THREADS 256u
+
+/* Back-reference copy of L bytes from distance `back` (src/lzf_d.c:137-142
+ * copies byte-serially, so an overlapping source replicates a period of
+ * `back` bytes).  Pieces of up to 16 bytes; while the period is shorter than
+ * 16 the copy distance doubles (any multiple of the period is a valid source
+ * once that many bytes exist), so a run of 264 takes 5 + 16 pieces. */
+__device__ __forceinline__ void ln_copy_back(uint8_t *out, uint32_t o, uint32_t back, uint32_t L,
+                                             uint32_t cap)
+{
+    uint32_t D = back, t = 0;
+    do {
+        uint32_t c = L - t;
+        if (c > 16u) c = 16u;
+        if (c > D) c = D;
+        const uint32_t s = o + t - D;
+        const uint4 v = ln_ld16_safe(out + s, cap - s);
+        ln_st_exact(out + o + t, v, c);
+        t += c;
+        if (D < 16u) D <<= 1;
+    } while (t < L);
+}
+
+__global__ __launch_bounds__(LD_THREADS) void lzf_decompress_lane_kernel(LzfBatch bt)
+{
+    const uint32_t v = blockIdx.x * LD_THREADS + threadIdx.x;
+    if (v >= bt.count) return;
+    if (bt.skip && bt.skip[v]) return;
+    const uint32_t in_len = bt.in_len[v];
+    const uint32_t cap = bt.out_cap[v];
+    const uint8_t *in = bt.in + bt.in_off[v];
+    uint8_t *out = bt.out + bt.out_off[v];
+    /* as the reference (do-while, src/lzf_d.c:64), a 0-length stream still
+     * reads its first control byte */
+    const uint32_t avail = in_len ? in_len : 1u;
+    uint32_t i = 0, o = 0;
+    int32_t err = 0;
+    do {
+        uint4 w0, w1;
+        if (i + 32u <= avail) {
+            w0 = ln_ld16(in + i);
+            w1 = ln_ld16(in + i + 16u);
+        } else {
+            w0 = ln_ld16_safe(in + i, avail - i);
+            w1 = i + 16u < avail ? ln_ld16_tail(in + i + 16u, avail - i - 16u) : make_uint4(0, 0, 0, 0);
+        }
+        const uint32_t c = w0.x & 0xFFu;
+        if (c < 32u) {                                               /* literal run */
+            const uint32_t cnt = c + 1u;
+            if ((uint64_t)o + cnt > cap) { err = 7; break; }         /* E2BIG  src/lzf_d.c:72 */
+            if ((uint64_t)i + 1u + cnt > in_len) { err = 22; break; }/* EINVAL src/lzf_d.c:79 */
+            const uint4 lo = make_uint4(ln_ab(w0.y, w0.x), ln_ab(w0.z, w0.y), ln_ab(w0.w, w0.z),
+                                        ln_ab(w1.x, w0.w));
+            ln_st_exact(out + o, lo, cnt);
+            if (cnt > 16u) {
+                const uint32_t b32 = cnt == 32u ? (uint32_t)in[i + 32u] : 0u;
+                const uint4 hi = make_uint4(ln_ab(w1.y, w1.x), ln_ab(w1.z, w1.y), ln_ab(w1.w, w1.z),
+                                            ln_ab(b32, w1.w));
+                ln_st_exact(out + o + 16u, hi, cnt - 16u);
+            }
+            o += cnt;
+            i += 1u + cnt;
+        } else {                                                     /* back-reference */
+            uint32_t len = c >> 5, ob = (w0.x >> 8) & 0xFFu, tsz = 2u;
+            if (i + 1u >= in_len) { err = 22; break; }               /* src/lzf_d.c:101 */
+            if (len == 7u) {
+                len += ob;
+                ob = (w0.x >> 16) & 0xFFu;
+                tsz = 3u;
+                if (i + 2u >= in_len) { err = 22; break; }           /* src/lzf_d.c:111 */
+            }
+            const uint32_t back = ((c & 31u) << 8) + 1u + ob;
+            if ((uint64_t)o + len + 2u > cap) { err = 7; break; }    /* src/lzf_d.c:121 */
+            if (back > o) { err = 22; break; }                       /* src/lzf_d.c:127 */
+            ln_copy_back(out, o, back, len + 2u, cap);
+            o += len + 2u;
+            i += tsz;
+        }
+    } while (i < in_len);
+    bt.out_len[v] = err ? 0u : o;
+    bt.err[v] = err;
+}
+
+hipError_t lzf_launch_decompress_lane(const LzfBatch &b, hipStream_t s)
+{
+    const uint32_t grid = (b.count + LD_THREADS - 1u) / LD_THREADS;
+    hipLaunchKernelGGL(lzf_decompress_lane_kernel, dim3(grid), dim3(LD_THREADS), 0, s, b);
+    return hipGetLastError();
+}
+
+/* ======================================================================== */
+/* compress, kernel 1: same-slot predecessor of every position              */
+/* ======================================================================== */
+
+/* cand word: bits 0-12 off = p - q - 1, bits 13-15 code:
+ *   0  no earlier position with p's slot inside the window (or only q = 0,
+ *      which is never a ref: src/lzf_c.c:155 `ref > in_data`)
+ *   1  q has p's slot but its 3 bytes differ (slot collision)
+ *   2..6  bytes agree for exactly code+1 bytes (3..7)
+ *   7  bytes agree for >= 8 bytes                                         */
+#define CAND_DIFF   1u
+#define CAND_LONG   7u
+
+#define K1_WIN      4u            /* windows of 64 positions resolved per step */
+#define KS_BUCKETS  4096u         /* small class: 12-bit bucket, 4-bit identity */
+#define KS_MAXN     4097u         /* positions + 1 fit 12 bits */
+#define KM_BUCKETS  2048u         /* mid class */
+#define KM_MAXN     65536u        /* positions + 1 fit 16 bits */
+
+__device__ __forceinline__ uint32_t k1_tri(const uint8_t *src, uint32_t n, uint32_t p)
+{
+    if (p + 4u <= n) return ln_ld4(src + p);
+    return (uint32_t)src[p] | ((uint32_t)src[p + 1u] << 8) | ((uint32_t)src[p + 2u] << 16);
+}
+
+/* agreement of the bytes at p and q (q < p), at most 8 and at most n - p */
+__device__ __forceinline__ uint32_t k1_agree(const uint8_t *src, uint32_t n, uint32_t p, uint32_t q)
+{
+    const uint32_t avail = n - p;
+    uint32_t a0, a1, b0, b1;
+    if (avail >= 8u) {
+        const uint2 a = ln_ld8(src + p), b = ln_ld8(src + q);
+        a0 = a.x; a1 = a.y; b0 = b.x; b1 = b.y;
+    } else {
+        const uint4 a = ln_ld16_tail(src + p, avail), b = ln_ld16_tail(src + q, avail);
+        a0 = a.x; a1 = a.y; b0 = b.x; b1 = b.y;
+    }
+    uint32_t k;
+    if (a0 != b0) k = (uint32_t)__builtin_ctz(a0 ^ b0) >> 3;
+    else if (a1 != b1) k = 4u + ((uint32_t)__builtin_ctz(a1 ^ b1) >> 3);
+    else k = 8u;
+    return k < avail ? k : avail;
+}
+
+__device__ __forceinline__ uint32_t k1_code(uint32_t k)
+{
+    return k < 3u ? CAND_DIFF : (k >= 8u ? CAND_LONG : k - 1u);
+}
+
+/* Lane-order check of the bucket-head atomics: a returned head from a later
+ * position means the LDS did not serialise the wave's same-address atomics in
+ * lane order; then the predecessors are rebuilt from the keys (the head before
+ * the step is the smallest value any lane of the bucket got back). */
+template <uint32_t BSHIFT>
+__device__ __noinline__ void k1_fix_order(uint32_t (&r)[K1_WIN], const uint32_t (&key)[K1_WIN],
+                                          const bool (&act)[K1_WIN])
+{
+    const uint32_t lane = threadIdx.x;
+    uint32_t fixed[K1_WIN];
+#pragma unroll
+    for (uint32_t j = 0; j < K1_WIN; j++) {
+        const uint32_t myb = (key[j] & 0xFFFFu) >> BSHIFT;
+        uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+        for (uint32_t t = 0; t < 64u * K1_WIN; t++) {
+            const uint32_t tj = t >> 6, tl = t & 63u;
+            uint32_t kt = 0u, rt = 0u, at = 0u;
+#pragma unroll
+            for (uint32_t jj = 0; jj < K1_WIN; jj++) {
+                const uint32_t kk = (uint32_t)__shfl((int)key[jj], (int)tl);
+                const uint32_t rr = (uint32_t)__shfl((int)r[jj], (int)tl);
+                const uint32_t aa = (uint32_t)__shfl(act[jj] ? 1 : 0, (int)tl);
+                if (jj == tj) { kt = kk; rt = rr; at = aa; }
+            }
+            if (at && ((kt & 0xFFFFu) >> BSHIFT) == myb) {
+                mn = rt < mn ? rt : mn;
+                if (t < 64u * j + lane && kt > mx) mx = kt;
+            }
+        }
+        fixed[j] = mn > mx ? mn : mx;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < K1_WIN; j++)
+        if (act[j]) r[j] = fixed[j];
+}
+
+/* Small class (every value <= KS_MAXN bytes: all positions inside one 8 KiB
+ * window).  LDS: bucket heads [pos+1:16 | mix:16] (16 KiB) and the bucket
+ * chain [pos+1 of the predecessor:12 | its identity:4] per position (8 KiB). */
+__global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLaneScratch sc)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t H[KS_BUCKETS];
+    __shared__ uint16_t E[KS_MAXN];
+    const uint32_t lane = threadIdx.x, v = blockIdx.x;
+    const uint32_t n = bt.in_len[v];
+    const uint8_t *src = bt.in + bt.in_off[v];
+    uint16_t *cand = sc.cand + (uint64_t)v * sc.cstride;
+    uint32_t *bits = sc.bits + (uint64_t)v * sc.bstride;
+    for (uint32_t w = lane; w < ((n + 31u) >> 5); w += 64u) bits[w] = 0u;
+    if (n < 3u) return;
+    for (uint32_t k = lane; k < KS_BUCKETS / 4u; k += 64u) ((uint4 *)H)[k] = make_uint4(0, 0, 0, 0);
+    ln_wave_fence();
+    const uint32_t np = n - 2u;                       /* positions 0 .. n-3 */
+    for (uint32_t P = 0; P < np; P += 64u * K1_WIN) {
+        uint32_t p[K1_WIN], m[K1_WIN], key[K1_WIN], r[K1_WIN];
+        bool act[K1_WIN];
+#pragma unroll
+        for (uint32_t j = 0; j < K1_WIN; j++) {
+            p[j] = P + 64u * j + lane;
+            act[j] = p[j] < np;
+            m[j] = act[j] ? ln_mix(ln_slot(k1_tri(src, n, p[j]))) : 0u;
+            key[j] = ((p[j] + 1u) << 16) | m[j];
+        }
+        /* in position order: window j's atomics after window j-1's (LDS ops
+         * of a wave execute in order), lanes of one instruction in lane order */
+#pragma unroll
+        for (uint32_t j = 0; j < K1_WIN; j++)
+            r[j] = act[j] ? atomicMax(&H[m[j] >> 4], key[j]) : 0u;
+        bool bad = sc.force_fix != 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < K1_WIN; j++) bad |= act[j] && (r[j] >> 16) > p[j];
+        if (__ballot(bad)) k1_fix_order<4>(r, key, act);
+#pragma unroll
+        for (uint32_t j = 0; j < K1_WIN; j++)
+            if (act[j]) E[p[j]] = (uint16_t)(((r[j] >> 16) << 4) | (r[j] & 15u));
+        ln_wave_fence();
+        /* walk the bucket chain to the latest position with the same slot */
+        uint32_t cp[K1_WIN];
+        bool fd[K1_WIN], need = false;
+#pragma unroll
+        for (uint32_t j = 0; j < K1_WIN; j++) {
+            cp[j] = r[j] >> 16;
+            fd[j] = cp[j] != 0u && (r[j] & 15u) == (m[j] & 15u);
+            need |= act[j] && !fd[j] && cp[j] != 0u;
+        }
+        while (__ballot(need)) {
+            need = false;
+#pragma unroll
+            for (uint32_t j = 0; j < K1_WIN; j++) {
+                if (act[j] && !fd[j] && cp[j] != 0u) {
+                    const uint32_t e = E[cp[j] - 1u];
+                    cp[j] = e >> 4;
+                    fd[j] = cp[j] != 0u && (e & 15u) == (m[j] & 15u);
+                    need |= !fd[j] && cp[j] != 0u;
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < K1_WIN; j++) {
+            if (!act[j]) continue;
+            uint32_t w = 0u;
+            if (fd[j] && cp[j] > 1u) {                   /* q = cp - 1 > 0 */
+                const uint32_t q = cp[j] - 1u;
+                w = (k1_code(k1_agree(src, n, p[j], q)) << 13) | (p[j] - q - 1u);
+            }
+            cand[p[j]] = (uint16_t)w;
+        }
+    }
+}
+
+/* Mid class (values <= 64 KiB).  LDS: bucket heads [pos+1:16 | mix:16]
+ * (8 KiB), a ring of the head each position displaced (its bucket
+ * predecessor's key) over the last 8192 positions (32 KiB), and the keys of
+ * the step in flight, which join the ring only after the step's walks. */
+__global__ __launch_bounds__(64) void lzf_cand_mid_kernel(LzfBatch bt, LzfLaneScratch sc)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t H[KM_BUCKETS];
+    __shared__ uint32_t R[LZF_WINDOW];
+    __shared__ uint32_t S[64u * K1_WIN];
+    const uint32_t lane = threadIdx.x, v = blockIdx.x;
+    const uint32_t n = bt.in_len[v];
+    const uint8_t *src = bt.in + bt.in_off[v];
+    uint16_t *cand = sc.cand + (uint64_t)v * sc.cstride;
+    uint32_t *bits = sc.bits + (uint64_t)v * sc.bstride;
+    for (uint32_t w = lane; w < ((n + 31u) >> 5); w += 64u) bits[w] = 0u;
+    if (n < 3u) return;
+    for (uint32_t k = lane; k < KM_BUCKETS / 4u; k += 64u) ((uint4 *)H)[k] = make_uint4(0, 0, 0, 0);
+    ln_wave_fence();
+    const uint32_t np = n - 2u;
+    for (uint32_t P = 0; P < np; P += 64u * K1_WIN) {
+        uint32_t p[K1_WIN], m[K1_WIN], key[K1_WIN], r[K1_WIN];
+        bool act[K1_WIN];
+#pragma unroll
+        for (uint32_t j = 0; j < K1_WIN; j++) {
+            p[j] = P + 64u * j + lane;
+            act[j] = p[j] < np;
+            m[j] = act[j] ? ln_mix(ln_slot(k1_tri(src, n, p[j]))) : 0u;
+            key[j] = ((p[j] + 1u) << 16) | m[j];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < K1_WIN; j++)
+            r[j] = act[j] ? atomicMax(&H[m[j] >> 5], key[j]) : 0u;
+        bool bad = sc.force_fix != 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < K1_WIN; j++) bad |= act[j] && (r[j] >> 16) > p[j];
+        if (__ballot(bad)) k1_fix_order<5>(r, key, act);
+#pragma unroll
+        for (uint32_t j = 0; j < K1_WIN; j++) S[64u * j + lane] = r[j];
+        ln_wave_fence();
+        uint32_t cur[K1_WIN];
+        bool fd[K1_WIN], need = false;
+#pragma unroll
+        for (uint32_t j = 0; j < K1_WIN; j++) {
+            cur[j] = r[j];
+            /* an entry is usable while inside the window: p - q - 1 < 8192 */
+            if (cur[j] && p[j] - (cur[j] >> 16) >= LZF_WINDOW) cur[j] = 0u;
+            fd[j] = cur[j] != 0u && (cur[j] & 0xFFFFu) == m[j];
+            need |= act[j] && !fd[j] && cur[j] != 0u;
+        }
+        while (__ballot(need)) {
+            need = false;
+#pragma unroll
+            for (uint32_t j = 0; j < K1_WIN; j++) {
+                if (act[j] && !fd[j] && cur[j] != 0u) {
+                    const uint32_t x = (cur[j] >> 16) - 1u;
+                    uint32_t e = x >= P ? S[x - P] : R[x & (LZF_WINDOW - 1u)];
+                    if (e && p[j] - (e >> 16) >= LZF_WINDOW) e = 0u;
+                    cur[j] = e;
+                    fd[j] = e != 0u && (e & 0xFFFFu) == m[j];
+                    need |= !fd[j] && e != 0u;
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < K1_WIN; j++) {
+            if (!act[j]) continue;
+            uint32_t w = 0u;
+            if (fd[j] && (cur[j] >> 16) > 1u) {
+                const uint32_t q = (cur[j] >> 16) - 1u;
+                w = (k1_code(k1_agree(src, n, p[j], q)) << 13) | (p[j] - q - 1u);
+            }
+            cand[p[j]] = (uint16_t)w;
+        }
+        ln_wave_fence();
+#pragma unroll
+        for (uint32_t j = 0; j < K1_WIN; j++)
+            if (act[j]) R[p[j] & (LZF_WINDOW - 1u)] = r[j];
+        ln_wave_fence();
+    }
+}
+
+/* ======================================================================== */
+/* compress, kernel 2: the greedy parse and emission, one lane per value    */
+/* ======================================================================== */
+
+#define K2_THREADS 256u
+
+/* Output in aligned dwords: `acc` holds the bytes from the aligned address
+ * `abase` on (accn of them; the ones before dst are never stored). */
+struct LnOut {
+    uint64_t acc;
+    uint32_t accn;
+    uint8_t *abase;
+    uint8_t *dst;
+
+    __device__ __forceinline__ void flush32(uint8_t *a, uint32_t w) const
+    {
+        if (a >= dst) {
+            *(uint32_t *)a = w;
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < 4u; k++)
+                if (a + k >= dst) a[k] = (uint8_t)(w >> (8u * k));
+        }
+    }
+    /* append cnt (1..3) bytes, little-endian in `bytes` */
+    __device__ __forceinline__ void put(uint32_t bytes, uint32_t cnt)
+    {
+        acc |= (uint64_t)bytes << (8u * accn);
+        accn += cnt;
+        if (accn >= 4u) {
+            flush32(abase, (uint32_t)acc);
+            acc >>= 32;
+            abase += 4;
+            accn -= 4u;
+        }
+    }
+    __device__ __forceinline__ uint8_t *wp() const { return abase + accn; }
+    __device__ __forceinline__ void patch(uint8_t *a, uint32_t byte)
+    {
+        if (a >= abase) {
+            const uint32_t sh = 8u * (uint32_t)(a - abase);
+            acc = (acc & ~(0xFFull << sh)) | ((uint64_t)byte << sh);
+        } else {
+            *a = (uint8_t)byte;
+        }
+    }
+    __device__ __forceinline__ void finish()
+    {
+        for (uint32_t k = 0; k < accn; k++)
+            if (abase + k >= dst) abase[k] = (uint8_t)(acc >> (8u * k));
+    }
+};
+
+/* m = min(first mismatch >= start, lim), bytes [0, start) known equal
+ * (src/lzf_c.c:169-209; lim carries the 16-compare quirk) */
+__device__ uint32_t ln_extend(const uint8_t *src, uint32_t n, uint32_t p, uint32_t q, uint32_t start,
+                              uint32_t lim)
+{
+    uint32_t k = start;
+    while (k < lim) {
+        const uint32_t avail = n - (p + k);
+        const uint4 a = ln_ld16_safe(src + p + k, avail), b = ln_ld16_safe(src + q + k, avail);
+        const uint32_t d = ln_first_diff(a, b);
+        k += d;
+        if (d < 16u) break;
+    }
+    return k < lim ? k : lim;
+}
+
+__global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt, LzfLaneScratch sc)
+{
+    const uint32_t v = blockIdx.x * K2_THREADS + threadIdx.x;
+    if (v >= bt.count) return;
+    const uint32_t n = bt.in_len[v], cap = bt.out_cap[v];
+    if (n == 0u || cap == 0u) { bt.out_len[v] = 0u; return; }        /* src/lzf_c.c:131 */
+    const uint8_t *src = bt.in + bt.in_off[v];
+    uint8_t *dst = bt.out + bt.out_off[v];
+    const uint16_t *cand = sc.cand + (uint64_t)v * sc.cstride;
+    uint32_t *bits = sc.bits + (uint64_t)v * sc.bstride;
+
+    LnOut E;
+    E.acc = 0;
+    E.accn = (uint32_t)((uintptr_t)dst & 3u);
+    E.abase = dst - E.accn;
+    E.dst = dst;
+    uint8_t *hp = dst;                 /* header byte of the open literal run */
+    uint32_t o = 1u, run = 0u, p = 0u; /* o, run: the reference's op and lit */
+    bool ok = true;
+
+    const uint8_t *wa = nullptr;       /* 16-byte input window (+ next one) */
+    uint4 W = make_uint4(0, 0, 0, 0), W2 = W;
+    uint32_t cb = 0xFFFFFFFFu;         /* cand entries [cb, cb+8) (+ next 8) */
+    uint4 C = W, C2 = W;
+    uint32_t cw = 0u, curw = 0u;       /* inserted-bitmap word of p, in flight */
+    uint32_t pw1 = 0u, pw2 = 0u, pw3 = 0u, pw4 = 0u;   /* words cw-1 .. cw-4 */
+    uint32_t ms = 0u, me = 0u;         /* the last match: [ms, me) */
+    const uint8_t *const src_end = src + n;
+
+#define LN_BYTE(pos, out_)                                                         \
+    do {                                                                           \
+        const uint8_t *a_ = src + (pos);                                           \
+        const uint8_t *al_ = (const uint8_t *)((uintptr_t)a_ & ~(uintptr_t)15);   \
+        if (al_ != wa) {                                                           \
+            W = al_ == wa + 16 ? W2 : *(const uint4 *)al_;                         \
+            if (al_ + 16 < src_end) W2 = *(const uint4 *)(al_ + 16);               \
+            wa = al_;                                                              \
+        }                                                                          \
+        const uint32_t o_ = (uint32_t)(a_ - al_);                                  \
+        (out_) = (ln_sel4(W, o_ >> 2) >> (8u * (o_ & 3u))) & 0xFFu;                \
+    } while (0)
+
+    while (n >= 3u && p < n - 2u) {                                   /* src/lzf_c.c:145 */
+        const uint32_t blk = p & ~7u;
+        if (blk != cb) {
+            C = blk == cb + 8u ? C2 : *(const uint4 *)(cand + blk);
+            C2 = *(const uint4 *)(cand + blk + 8u);                   /* scratch has slack */
+            cb = blk;
+        }
+        const uint32_t c = (ln_sel4(C, (p >> 1) & 3u) >> (16u * (p & 1u))) & 0xFFFFu;
+        /* rel: 0 no ref; 1 ref with other bytes; 2..6 equal for rel+1 bytes;
+         * 7 equal >= 8 bytes; 8 equal 3 bytes, length unknown; 9 unknown */
+        uint32_t rel = c >> 13;
+        uint32_t q = p - 1u - (c & 0x1FFFu);
+        if (rel) {
+            for (;;) {
+                bool ins;
+                if (q >= ms) {
+                    ins = !(q > ms && q + 3u <= me);                  /* interior of the last match */
+                } else {
+                    const uint32_t d = cw - (q >> 5);
+                    const uint32_t word = d == 0u ? curw : d == 1u ? pw1 : d == 2u ? pw2 :
+                                          d == 3u ? pw3 : d == 4u ? pw4 : bits[q >> 5];
+                    ins = (word >> (q & 31u)) & 1u;
+                }
+                if (ins) break;                                       /* q inserted: it is the ref */
+                const uint32_t c2 = cand[q];
+                const uint32_t r2 = c2 >> 13;
+                const uint32_t q2 = q - 1u - (c2 & 0x1FFFu);
+                if (!r2 || p - q2 - 1u >= LZF_WINDOW) { rel = 0u; break; }
+                const bool e1 = rel >= 2u && rel <= 8u, e2 = r2 >= 2u;
+                rel = rel == 9u ? 9u : (e1 && e2) ? 8u : (e1 != e2) ? 1u : 9u;
+                q = q2;
+            }
+            if (rel == 9u)
+                rel = (src[q] == src[p] && src[q + 1u] == src[p + 1u] && src[q + 2u] == src[p + 2u]) ? 8u : 1u;
+        }
+        const bool hit = rel >= 2u && p + 4u < n;                    /* src/lzf_c.c:151-166 */
+        curw |= 1u << (p & 31u);                                     /* p is inserted */
+        if (!hit) {
+            if (o >= cap) { ok = false; break; }                     /* src/lzf_c.c:263 */
+            uint32_t byte;
+            LN_BYTE(p, byte);
+            if (run == 0u) { hp = E.wp(); E.put(byte << 8, 2u); }    /* header placeholder */
+            else E.put(byte, 1u);
+            o++;
+            if (++run == LZF_MAX_LIT) { E.patch(hp, LZF_MAX_LIT - 1u); run = 0u; o++; }
+            p++;
+            if ((p & 31u) == 0u) {
+                bits[cw] = curw;
+                pw4 = pw3; pw3 = pw2; pw2 = pw1; pw1 = curw;
+                cw++;
+                curw = 0u;
+            }
+            continue;
+        }
+        uint32_t maxlen = n - p - 2u;                                /* src/lzf_c.c:169-170 */
+        if (maxlen > LZF_MAX_REF) maxlen = LZF_MAX_REF;
+        const uint32_t lim = (maxlen > 16u && maxlen < 19u) ? 19u : maxlen;
+        uint32_t m;
+        if (rel <= 6u) {
+            m = rel + 1u;
+            if (m > lim) m = lim;
+        } else {
+            m = ln_extend(src, n, p, q, rel == 7u ? 8u : 3u, lim);
+        }
+        const uint32_t off = p - q - 1u;
+        if (run) E.patch(hp, run - 1u);                              /* close the run */
+        else o--;                                                    /* undo empty run */
+        if (o + 4u >= cap) { ok = false; break; }                    /* src/lzf_c.c:176 */
+        const uint32_t L = m - 2u;
+        if (L < 7u) {
+            E.put(((off >> 8) | (L << 5)) | ((off & 0xFFu) << 8), 2u);
+            o += 2u;
+        } else {
+            E.put((0xE0u | (off >> 8)) | ((L - 7u) << 8) | ((off & 0xFFu) << 16), 3u);
+            o += 3u;
+        }
+        run = 0u;
+        o++;                                                         /* reserve a header */
+        ms = p;
+        p += m;
+        me = p;
+        if (p >= n - 2u) break;                                      /* src/lzf_c.c:229 */
+        /* the two last positions of the match are inserted, its interior not */
+        const uint32_t nw = p >> 5, t1 = p - 2u, t2 = p - 1u;
+        const uint32_t b1 = 1u << (t1 & 31u), b2 = 1u << (t2 & 31u);
+        if (nw == cw) {
+            curw |= b1 | b2;
+        } else {
+            uint32_t wo = curw, wm = 0u, wn = 0u;
+            if ((t1 >> 5) == cw) wo |= b1; else if ((t1 >> 5) == nw) wn |= b1; else wm |= b1;
+            if ((t2 >> 5) == cw) wo |= b2; else if ((t2 >> 5) == nw) wn |= b2; else wm |= b2;
+            bits[cw] = wo;
+            if (wm) bits[nw - 1u] = wm;
+            const uint32_t d = nw - cw;          /* words cw+1 .. nw-2 stay all-interior (0) */
+            const uint32_t n1 = d == 1u ? wo : wm;
+            const uint32_t n2 = d == 1u ? pw1 : d == 2u ? wo : 0u;
+            const uint32_t n3 = d == 1u ? pw2 : d == 2u ? pw1 : d == 3u ? wo : 0u;
+            const uint32_t n4 = d == 1u ? pw3 : d == 2u ? pw2 : d == 3u ? pw1 : d == 4u ? wo : 0u;
+            pw1 = n1; pw2 = n2; pw3 = n3; pw4 = n4;
+            curw = wn;
+            cw = nw;
+        }
+    }
+    if (!ok || o + 3u > cap) { bt.out_len[v] = 0u; return; }          /* src/lzf_c.c:276 */
+    while (p < n) {                                                   /* src/lzf_c.c:279-288 */
+        uint32_t byte;
+        LN_BYTE(p, byte);
+        if (run == 0u) { hp = E.wp(); E.put(byte << 8, 2u); }
+        else E.put(byte, 1u);
+        o++;
+        if (++run == LZF_MAX_LIT) { E.patch(hp, LZF_MAX_LIT - 1u); run = 0u; o++; }
+        p++;
+    }
+#undef LN_BYTE
+    if (run) E.patch(hp, run - 1u);
+    else o--;
+    E.finish();
+    bt.out_len[v] = o;
+}
+
+/* ---- launcher ------------------------------------------------------------ */
+
+static uint64_t lane_cstride(uint32_t max_len) { return (((uint64_t)max_len + 7u) & ~7ull) + 8u; }
+static uint64_t lane_bstride(uint32_t max_len) { return ((((uint64_t)max_len + 31u) >> 5) + 3u) & ~3ull; }
+
+size_t lzf_lane_scratch_per_value(uint32_t max_len)
+{
+    return (size_t)(lane_cstride(max_len) * 2u + lane_bstride(max_len) * 4u);
+}
+
+bool lzf_lane_compress_supported(uint32_t max_len) { return max_len <= KM_MAXN; }
+
+hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scratch,
+                                    size_t scratch_bytes, uint32_t force_fix)
+{
+    if (b.max_len > KM_MAXN) return hipErrorInvalidValue;
+    const uint64_t cstride = lane_cstride(b.max_len), bstride = lane_bstride(b.max_len);
+    uint64_t chunk = scratch_bytes / lzf_lane_scratch_per_value(b.max_len);
+    const auto bits_at = [&](uint64_t ch) { return ((ch * cstride * 2u) + 255u) & ~255ull; };
+    while (chunk && bits_at(chunk) + chunk * bstride * 4u > scratch_bytes) chunk--;
+    if (chunk == 0) return hipErrorInvalidValue;
+    LzfLaneScratch sc;
+    sc.cand = (uint16_t *)scratch;
+    sc.bits = (uint32_t *)((uint8_t *)scratch + bits_at(chunk));
+    sc.cstride = cstride;
+    sc.bstride = bstride;
+    sc.force_fix = force_fix;
+    for (uint64_t first = 0; first < b.count; first += chunk) {
+        const uint32_t cnt = (uint32_t)((b.count - first) < chunk ? (b.count - first) : chunk);
+        LzfBatch c = b;
+        c.in_off = b.in_off + first;
+        c.in_len = b.in_len + first;
+        c.out_off = b.out_off + first;
+        c.out_cap = b.out_cap + first;
+        c.out_len = b.out_len + first;
+        c.count = cnt;
+        if (b.max_len <= KS_MAXN)
+            hipLaunchKernelGGL(lzf_cand_small_kernel, dim3(cnt), dim3(64), 0, s, c, sc);
+        else
+            hipLaunchKernelGGL(lzf_cand_mid_kernel, dim3(cnt), dim3(64), 0, s, c, sc);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(lzf_parse_lane_kernel, dim3((cnt + K2_THREADS - 1u) / K2_THREADS),
+                           dim3(K2_THREADS), 0, s, c, sc);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}

@@ -26,9 +26,9 @@ def _caps_layout(caps, align=16):
     return np.array(offs, np.int64), max(pos, 16)
 
 
-def gpu_compress(values, out_caps, dev="cuda"):
-    arena, in_off = _pack(values)
-    out_off, out_size = _caps_layout(out_caps)
+def gpu_compress(values, out_caps, dev="cuda", align=16):
+    arena, in_off = _pack(values, align)
+    out_off, out_size = _caps_layout(out_caps, align)
     d_in = torch.from_numpy(arena).to(dev)
     d_in_off = torch.from_numpy(in_off).to(dev)
     d_in_len = torch.tensor([len(v) for v in values], dtype=torch.int32, device=dev)
@@ -47,9 +47,9 @@ def gpu_compress(values, out_caps, dev="cuda"):
     return res
 
 
-def gpu_decompress(streams, out_caps, dev="cuda"):
-    arena, in_off = _pack(streams)
-    out_off, out_size = _caps_layout(out_caps)
+def gpu_decompress(streams, out_caps, dev="cuda", align=16):
+    arena, in_off = _pack(streams, align)
+    out_off, out_size = _caps_layout(out_caps, align)
     d_in = torch.from_numpy(arena).to(dev)
     d_in_off = torch.from_numpy(in_off).to(dev)
     d_in_len = torch.tensor([len(v) for v in streams], dtype=torch.int32, device=dev)

@@ -17,15 +17,15 @@ from tests.oracle_lib import sha16, synth
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-GENERATIONS = ["parallel", "serial"]
+GENERATIONS = ["lane", "window", "serial"]
 
 
 @pytest.fixture(params=GENERATIONS)
 def generation(request, monkeypatch):
-    if request.param == "serial":
-        monkeypatch.setenv("LZF_GPU_KERNEL", "serial")
-    else:
+    if request.param == "lane":
         monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    else:
+        monkeypatch.setenv("LZF_GPU_KERNEL", request.param)
     return request.param
 
 
@@ -98,9 +98,43 @@ def test_batch_decompress_golden(golden, oracle):
     assert not bad, f"{len(bad)} mismatches, first: {bad[:5]}"
 
 
-def test_batch_decompress_serial_generation(golden, oracle, monkeypatch):
-    monkeypatch.setenv("LZF_GPU_KERNEL", "serial")
+@pytest.mark.parametrize("gen", ["window", "serial"])
+def test_batch_decompress_other_generations(golden, oracle, monkeypatch, gen):
+    monkeypatch.setenv("LZF_GPU_KERNEL", gen)
     test_batch_decompress_golden(golden, oracle)
+
+
+@pytest.mark.parametrize("align", [1, 3])
+def test_unaligned_arenas(oracle, generation, align):
+    # values, streams and outputs at arbitrary byte offsets of their arenas
+    from tests.gpu_batch import gpu_compress, gpu_decompress
+    rnd = random.Random(align)
+    vals, caps = [], []
+    for i in range(600):
+        n = rnd.choice([1, 2, 3, 4, 5, 17, 33, 64, 700, 4096, 5003])
+        vals.append(synth(rnd.randrange(6), 0x5EED00C0, i, n))
+        caps.append(rnd.choice([max(1, n - 4), n + n // 16 + 64, rnd.randint(1, n + 8)]))
+    res = gpu_compress(vals, caps, align=align)
+    exp = [oracle.compress(v, c) for v, c in zip(vals, caps)]
+    bad = [i for i, (a, b) in enumerate(zip(res, exp)) if a != b]
+    assert not bad, f"{len(bad)} mismatches; first {bad[:5]}"
+    streams = [r for r in exp if r]
+    origs = [v for v, r in zip(vals, exp) if r]
+    assert gpu_decompress(streams, [len(v) for v in origs], align=align) == [(v, 0) for v in origs]
+
+
+def test_lane_order_repair_path(oracle, monkeypatch):
+    # the repair path of the bucket-head atomics (taken when the LDS does not
+    # serialise a wave's same-address atomics in lane order) gives the same
+    # streams
+    from tests.gpu_batch import gpu_compress
+    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.setenv("LZF_GPU_LANE_FORCE_FIX", "1")
+    rnd = random.Random(3)
+    for nmax in (4096, 20000):
+        vals = [synth(rnd.randrange(6), 0x5EED00D0, i, rnd.randint(1, nmax)) for i in range(200)]
+        caps = [max(1, len(v) - 4) for v in vals]
+        assert gpu_compress(vals, caps) == [oracle.compress(v, c) for v, c in zip(vals, caps)]
 
 
 @pytest.mark.parametrize("nmax", [8192, 9000])
