@@ -251,7 +251,7 @@ hipError_t lzf_launch_decompress_lane(const LzfBatch &b, hipStream_t s)
 
 #define K1_WIN      4u            /* windows of 64 positions resolved per step */
 #define KS_BUCKETS  4096u         /* small class: 12-bit bucket, 4-bit identity */
-#define KS_MAXN     4097u         /* positions + 1 fit 12 bits */
+#define KS_MAXN     4096u         /* staged whole; positions + 1 fit 12 bits */
 #define KM_BUCKETS  2048u         /* mid class */
 #define KM_MAXN     65536u        /* positions + 1 fit 16 bits */
 
@@ -322,76 +322,171 @@ __device__ __noinline__ void k1_fix_order(uint32_t (&r)[K1_WIN], const uint32_t 
 }
 
 /* Small class (every value <= KS_MAXN bytes: all positions inside one 8 KiB
- * window).  LDS: bucket heads [pos+1:16 | mix:16] (16 KiB) and the bucket
- * chain [pos+1 of the predecessor:12 | its identity:4] per position (8 KiB). */
+ * window).  Persistent workgroups of one wave walk the batch; the next
+ * value's bytes are loaded into registers while the current one is
+ * processed and then staged in LDS, so the position loop reads only LDS.
+ *
+ * Slot-mix m = mix(slot) (bijective): bucket = m >> 4, identity = m & 15.
+ * Per window of 64 positions, lanes with the same bucket / the same slot are
+ * found exactly with lane bitmaps keyed by m's digits [4,10), [10,16) and
+ * [0,4) (ds_or_b64, AND of the read-backs).  Per position the kernel keeps,
+ * in LDS, the bucket head (latest position of the bucket) and a skip link:
+ * the latest earlier position of the bucket with ANOTHER identity.  The
+ * same-slot predecessor is then the nearest same-slot lane below, else found
+ * from the head by following skip links until the identity matches (one hop
+ * per change of identity, not per position).  Entries are [pos+1:12 |
+ * identity:4].  LDS: heads 8 KiB, links 8 KiB, bytes 4 KiB, bitmaps 2.3 KiB. */
+__device__ __forceinline__ uint32_t ks_rd4(const uint32_t *w, uint32_t x)
+{
+    return __builtin_amdgcn_alignbyte(w[(x >> 2) + 1u], w[x >> 2], x & 3u);
+}
+
+/* highest set bit of a 64-bit mask (mask != 0) */
+__device__ __forceinline__ uint32_t ks_hibit(uint64_t m)
+{
+    return 63u - (uint32_t)__builtin_clzll(m);
+}
+
+#define KS_T0 0u      /* digit m[4,10)  : 64 entries */
+#define KS_T1 64u     /* digit m[10,16) : 64 entries */
+#define KS_T2 128u    /* digit m[0,4)   : 16 entries */
+#define KS_TN 144u
+
 __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLaneScratch sc)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t H[KS_BUCKETS];
+    __shared__ __attribute__((aligned(16))) uint16_t H[KS_BUCKETS];
     __shared__ uint16_t E[KS_MAXN];
-    const uint32_t lane = threadIdx.x, v = blockIdx.x;
-    const uint32_t n = bt.in_len[v];
-    const uint8_t *src = bt.in + bt.in_off[v];
-    uint16_t *cand = sc.cand + (uint64_t)v * sc.cstride;
-    uint32_t *bits = sc.bits + (uint64_t)v * sc.bstride;
-    for (uint32_t w = lane; w < ((n + 31u) >> 5); w += 64u) bits[w] = 0u;
-    if (n < 3u) return;
-    for (uint32_t k = lane; k < KS_BUCKETS / 4u; k += 64u) ((uint4 *)H)[k] = make_uint4(0, 0, 0, 0);
-    ln_wave_fence();
-    const uint32_t np = n - 2u;                       /* positions 0 .. n-3 */
-    for (uint32_t P = 0; P < np; P += 64u * K1_WIN) {
-        uint32_t p[K1_WIN], m[K1_WIN], key[K1_WIN], r[K1_WIN];
-        bool act[K1_WIN];
+    __shared__ __attribute__((aligned(16))) uint32_t Bw[KS_MAXN / 4u + 4u];
+    __shared__ unsigned long long T[K1_WIN][KS_TN];
+    const uint32_t lane = threadIdx.x;
+    const unsigned long long mine = 1ull << lane, below = mine - 1ull;
+    uint32_t v = blockIdx.x;
+    if (v >= bt.count) return;
+    for (uint32_t k = lane; k < K1_WIN * KS_TN; k += 64u) (&T[0][0])[k] = 0ull;
+    uint4 pf[4];
+    uint32_t pn = bt.in_len[v];
+    {
+        const uint8_t *s0 = bt.in + bt.in_off[v];
 #pragma unroll
-        for (uint32_t j = 0; j < K1_WIN; j++) {
-            p[j] = P + 64u * j + lane;
-            act[j] = p[j] < np;
-            m[j] = act[j] ? ln_mix(ln_slot(k1_tri(src, n, p[j]))) : 0u;
-            key[j] = ((p[j] + 1u) << 16) | m[j];
+        for (uint32_t k = 0; k < 4u; k++) {
+            const uint32_t at = 16u * (64u * k + lane);
+            pf[k] = at < pn ? ln_ld16_safe(s0 + at, pn - at) : make_uint4(0, 0, 0, 0);
         }
-        /* in position order: window j's atomics after window j-1's (LDS ops
-         * of a wave execute in order), lanes of one instruction in lane order */
+    }
+    while (v < bt.count) {
+        const uint32_t n = pn;
+        uint16_t *cand = sc.cand + (uint64_t)v * sc.cstride;
+        uint32_t *bits = sc.bits + (uint64_t)v * sc.bstride;
 #pragma unroll
-        for (uint32_t j = 0; j < K1_WIN; j++)
-            r[j] = act[j] ? atomicMax(&H[m[j] >> 4], key[j]) : 0u;
-        bool bad = sc.force_fix != 0u;
+        for (uint32_t k = 0; k < 4u; k++) ((uint4 *)Bw)[64u * k + lane] = pf[k];
+        const uint32_t vn = v + gridDim.x;
+        if (vn < bt.count) {                       /* next value's bytes, in flight */
+            pn = bt.in_len[vn];
+            const uint8_t *s1 = bt.in + bt.in_off[vn];
 #pragma unroll
-        for (uint32_t j = 0; j < K1_WIN; j++) bad |= act[j] && (r[j] >> 16) > p[j];
-        if (__ballot(bad)) k1_fix_order<4>(r, key, act);
-#pragma unroll
-        for (uint32_t j = 0; j < K1_WIN; j++)
-            if (act[j]) E[p[j]] = (uint16_t)(((r[j] >> 16) << 4) | (r[j] & 15u));
-        ln_wave_fence();
-        /* walk the bucket chain to the latest position with the same slot */
-        uint32_t cp[K1_WIN];
-        bool fd[K1_WIN], need = false;
-#pragma unroll
-        for (uint32_t j = 0; j < K1_WIN; j++) {
-            cp[j] = r[j] >> 16;
-            fd[j] = cp[j] != 0u && (r[j] & 15u) == (m[j] & 15u);
-            need |= act[j] && !fd[j] && cp[j] != 0u;
+            for (uint32_t k = 0; k < 4u; k++) {
+                const uint32_t at = 16u * (64u * k + lane);
+                pf[k] = at < pn ? ln_ld16_safe(s1 + at, pn - at) : make_uint4(0, 0, 0, 0);
+            }
         }
-        while (__ballot(need)) {
-            need = false;
+        for (uint32_t w = lane; w < ((n + 31u) >> 5); w += 64u) bits[w] = 0u;
+        if (n >= 3u) {
+            for (uint32_t k = lane; k < KS_BUCKETS / 8u; k += 64u) ((uint4 *)H)[k] = make_uint4(0, 0, 0, 0);
+            ln_wave_fence();
+            const uint32_t np = n - 2u;               /* positions 0 .. n-3 */
+            for (uint32_t P = 0; P < np; P += 64u * K1_WIN) {
+                uint32_t p[K1_WIN], m[K1_WIN], tri[K1_WIN];
+                bool act[K1_WIN];
 #pragma unroll
-            for (uint32_t j = 0; j < K1_WIN; j++) {
-                if (act[j] && !fd[j] && cp[j] != 0u) {
-                    const uint32_t e = E[cp[j] - 1u];
-                    cp[j] = e >> 4;
-                    fd[j] = cp[j] != 0u && (e & 15u) == (m[j] & 15u);
-                    need |= !fd[j] && cp[j] != 0u;
+                for (uint32_t j = 0; j < K1_WIN; j++) {
+                    p[j] = P + 64u * j + lane;
+                    act[j] = p[j] < np;
+                    tri[j] = ks_rd4(Bw, act[j] ? p[j] : 0u);
+                    m[j] = ln_mix(ln_slot(tri[j]));
+                    if (act[j]) {
+                        __hip_atomic_fetch_or(&T[j][KS_T0 + ((m[j] >> 4) & 63u)], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_or(&T[j][KS_T1 + (m[j] >> 10)], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_or(&T[j][KS_T2 + (m[j] & 15u)], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                ln_wave_fence();
+                unsigned long long MB[K1_WIN], MS[K1_WIN];
+#pragma unroll
+                for (uint32_t j = 0; j < K1_WIN; j++) {
+                    MB[j] = T[j][KS_T0 + ((m[j] >> 4) & 63u)] & T[j][KS_T1 + (m[j] >> 10)];
+                    MS[j] = MB[j] & T[j][KS_T2 + (m[j] & 15u)];
+                    if (!act[j]) MB[j] = MS[j] = 0ull;
+                }
+                ln_wave_fence();
+#pragma unroll
+                for (uint32_t j = 0; j < K1_WIN; j++) {
+                    if (act[j]) {
+                        T[j][KS_T0 + ((m[j] >> 4) & 63u)] = 0ull;
+                        T[j][KS_T1 + (m[j] >> 10)] = 0ull;
+                        T[j][KS_T2 + (m[j] & 15u)] = 0ull;
+                    }
+                }
+                /* window j reads the heads after window j-1 wrote them (LDS
+                 * ops of a wave execute in order) */
+                uint32_t q1[K1_WIN], cur[K1_WIN];
+                bool need = false;
+#pragma unroll
+                for (uint32_t j = 0; j < K1_WIN; j++) {
+                    const uint32_t bk = m[j] >> 4, id = m[j] & 15u;
+                    const uint32_t key = ((p[j] + 1u) << 4) | id;
+                    const unsigned long long ss = MS[j] & below, sb = MB[j] & ~MS[j] & below;
+                    const uint32_t h = act[j] ? (uint32_t)H[bk] : 0u;
+                    const uint32_t eh = (act[j] && h) ? (uint32_t)E[(h >> 4) - 1u] : 0u;
+                    /* skip link: latest earlier bucket position with another identity */
+                    const uint32_t lsb = sb ? ks_hibit(sb) : lane;
+                    const uint32_t ksb = (uint32_t)__shfl((int)key, (int)lsb);
+                    const uint32_t link = sb ? ksb : ((h & 15u) != id ? h : eh);
+                    if (act[j]) E[p[j]] = (uint16_t)link;
+                    if (act[j] && (MB[j] >> lane) == 1ull) H[bk] = (uint16_t)key;
+                    /* same-slot predecessor */
+                    q1[j] = ss ? P + 64u * j + ks_hibit(ss) + 1u : 0u;    /* pos+1 */
+                    cur[j] = (act[j] && !ss) ? h : 0u;
+                    if (cur[j] && (cur[j] & 15u) == id) { q1[j] = cur[j] >> 4; cur[j] = 0u; }
+                    need |= cur[j] != 0u;
+                }
+                ln_wave_fence();
+                while (__ballot(need)) {
+                    need = false;
+#pragma unroll
+                    for (uint32_t j = 0; j < K1_WIN; j++) {
+                        if (cur[j]) {
+                            const uint32_t e = E[(cur[j] >> 4) - 1u];
+                            cur[j] = e;
+                            if (e && (e & 15u) == (m[j] & 15u)) { q1[j] = e >> 4; cur[j] = 0u; }
+                            need |= cur[j] != 0u;
+                        }
+                    }
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < K1_WIN; j++) {
+                    if (!act[j]) continue;
+                    uint32_t w = 0u;
+                    if (q1[j] > 1u) {                    /* q = q1 - 1 > 0 */
+                        const uint32_t q = q1[j] - 1u;
+                        /* agreement of the bytes at p and q, <= 8, <= n - p */
+                        const uint32_t x0 = tri[j] ^ ks_rd4(Bw, q);
+                        uint32_t k;
+                        if (x0) {
+                            k = (uint32_t)__builtin_ctz(x0) >> 3;
+                        } else {
+                            const uint32_t x1 = ks_rd4(Bw, p[j] + 4u) ^ ks_rd4(Bw, q + 4u);
+                            k = x1 ? 4u + ((uint32_t)__builtin_ctz(x1) >> 3) : 8u;
+                        }
+                        const uint32_t avail = n - p[j];
+                        if (k > avail) k = avail;
+                        w = (k1_code(k) << 13) | (p[j] - q - 1u);
+                    }
+                    cand[p[j]] = (uint16_t)w;
                 }
             }
         }
-#pragma unroll
-        for (uint32_t j = 0; j < K1_WIN; j++) {
-            if (!act[j]) continue;
-            uint32_t w = 0u;
-            if (fd[j] && cp[j] > 1u) {                   /* q = cp - 1 > 0 */
-                const uint32_t q = cp[j] - 1u;
-                w = (k1_code(k1_agree(src, n, p[j], q)) << 13) | (p[j] - q - 1u);
-            }
-            cand[p[j]] = (uint16_t)w;
-        }
+        ln_wave_fence();
+        v = vn;
     }
 }
 
@@ -734,6 +829,22 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
     sc.cstride = cstride;
     sc.bstride = bstride;
     sc.force_fix = force_fix;
+    /* the small-class kernel is persistent: as many one-wave workgroups as
+     * stay resident (LDS-bound), each walking the batch */
+    uint32_t small_grid = 256u * 8u;
+    {
+        int dev = 0, cus = 0;
+        hipFuncAttributes fa;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            hipFuncGetAttributes(&fa, (const void *)lzf_cand_small_kernel) == hipSuccess && cus > 0 &&
+            fa.sharedSizeBytes > 0) {
+            uint32_t per = (uint32_t)(160u * 1024u / fa.sharedSizeBytes);   /* LDS-bound residency */
+            if (per > 32u) per = 32u;
+            if (per < 1u) per = 1u;
+            small_grid = (uint32_t)cus * per;
+        }
+    }
     for (uint64_t first = 0; first < b.count; first += chunk) {
         const uint32_t cnt = (uint32_t)((b.count - first) < chunk ? (b.count - first) : chunk);
         LzfBatch c = b;
@@ -743,8 +854,10 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
         c.out_cap = b.out_cap + first;
         c.out_len = b.out_len + first;
         c.count = cnt;
-        if (b.max_len <= KS_MAXN)
-            hipLaunchKernelGGL(lzf_cand_small_kernel, dim3(cnt), dim3(64), 0, s, c, sc);
+        if (b.max_len <= KS_MAXN) {
+            const uint32_t g = cnt < small_grid ? cnt : small_grid;
+            hipLaunchKernelGGL(lzf_cand_small_kernel, dim3(g), dim3(64), 0, s, c, sc);
+        }
         else
             hipLaunchKernelGGL(lzf_cand_mid_kernel, dim3(cnt), dim3(64), 0, s, c, sc);
         hipError_t e = hipGetLastError();
