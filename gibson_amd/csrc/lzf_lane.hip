@@ -577,68 +577,16 @@ __global__ __launch_bounds__(64) void lzf_cand_mid_kernel(LzfBatch bt, LzfLaneSc
 
 #define K2_THREADS 256u
 
-/* Output in aligned dwords: `acc` holds the bytes from the aligned address
- * `abase` on (accn of them; the ones before dst are never stored). */
-struct LnOut {
-    uint64_t acc;
-    uint32_t accn;
-    uint8_t *abase;
-    uint8_t *dst;
-
-    __device__ __forceinline__ void flush32(uint8_t *a, uint32_t w) const
-    {
-        if (a >= dst) {
-            *(uint32_t *)a = w;
-        } else {
-#pragma unroll
-            for (uint32_t k = 0; k < 4u; k++)
-                if (a + k >= dst) a[k] = (uint8_t)(w >> (8u * k));
-        }
-    }
-    /* append cnt (1..3) bytes, little-endian in `bytes` */
-    __device__ __forceinline__ void put(uint32_t bytes, uint32_t cnt)
-    {
-        acc |= (uint64_t)bytes << (8u * accn);
-        accn += cnt;
-        if (accn >= 4u) {
-            flush32(abase, (uint32_t)acc);
-            acc >>= 32;
-            abase += 4;
-            accn -= 4u;
-        }
-    }
-    __device__ __forceinline__ uint8_t *wp() const { return abase + accn; }
-    __device__ __forceinline__ void patch(uint8_t *a, uint32_t byte)
-    {
-        if (a >= abase) {
-            const uint32_t sh = 8u * (uint32_t)(a - abase);
-            acc = (acc & ~(0xFFull << sh)) | ((uint64_t)byte << sh);
-        } else {
-            *a = (uint8_t)byte;
-        }
-    }
-    __device__ __forceinline__ void finish()
-    {
-        for (uint32_t k = 0; k < accn; k++)
-            if (abase + k >= dst) abase[k] = (uint8_t)(acc >> (8u * k));
-    }
-};
-
 /* m = min(first mismatch >= start, lim), bytes [0, start) known equal
  * (src/lzf_c.c:169-209; lim carries the 16-compare quirk) */
-__device__ uint32_t ln_extend(const uint8_t *src, uint32_t n, uint32_t p, uint32_t q, uint32_t start,
-                              uint32_t lim)
-{
-    uint32_t k = start;
-    while (k < lim) {
-        const uint32_t avail = n - (p + k);
-        const uint4 a = ln_ld16_safe(src + p + k, avail), b = ln_ld16_safe(src + q + k, avail);
-        const uint32_t d = ln_first_diff(a, b);
-        k += d;
-        if (d < 16u) break;
-    }
-    return k < lim ? k : lim;
-}
+
+/* The lanes of a wave are at different points of their values, so the loop
+ * is a state machine in which every lane does at most ONE unit of each kind
+ * of work per iteration -- take the cand word of p, test one candidate for
+ * insertion (or hop one link back), compare one 16-byte piece of a long
+ * match, emit one literal or one back-reference -- and a long walk or match
+ * of one lane costs the others only the small blocks it runs through. */
+enum { K2_STEP = 0, K2_RESOLVE = 1, K2_DECIDE = 2, K2_EXTEND = 3, K2_EMIT = 4, K2_DONE = 5 };
 
 __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt, LzfLaneScratch sc)
 {
@@ -651,155 +599,232 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
     const uint16_t *cand = sc.cand + (uint64_t)v * sc.cstride;
     uint32_t *bits = sc.bits + (uint64_t)v * sc.bstride;
 
-    LnOut E;
-    E.acc = 0;
-    E.accn = (uint32_t)((uintptr_t)dst & 3u);
-    E.abase = dst - E.accn;
-    E.dst = dst;
-    uint8_t *hp = dst;                 /* header byte of the open literal run */
-    uint32_t o = 1u, run = 0u, p = 0u; /* o, run: the reference's op and lit */
-    bool ok = true;
-
-    const uint8_t *wa = nullptr;       /* 16-byte input window (+ next one) */
+    /* output: aligned dwords at da; acc holds the bytes from dword fw on */
+    const uint32_t dm = (uint32_t)((uintptr_t)dst & 3u);
+    uint8_t *const da = dst - dm;
+    uint64_t acc = 0;
+    uint32_t accn = dm, fw = 0;
+    uint32_t hx = dm;                   /* header byte of the open run (index from da) */
+    /* input: 16-byte window of aligned block wb (+ the next block) */
+    const uint32_t sm = (uint32_t)((uintptr_t)src & 15u);
+    const uint8_t *const sa = src - sm;
+    const uint32_t last_blk = (sm + n - 1u) >> 4;
+    uint32_t wb = 0xFFFFFFF0u;          /* no block yet (wb + 1 is no block either) */
     uint4 W = make_uint4(0, 0, 0, 0), W2 = W;
-    uint32_t cb = 0xFFFFFFFFu;         /* cand entries [cb, cb+8) (+ next 8) */
+
+    uint32_t o = 1u, run = 0u, p = 0u; /* o, run: the reference's op and lit */
+    uint32_t cb = 0xFFFFFFF0u;         /* cand entries [cb, cb+8) (+ next 8); none yet */
     uint4 C = W, C2 = W;
     uint32_t cw = 0u, curw = 0u;       /* inserted-bitmap word of p, in flight */
     uint32_t pw1 = 0u, pw2 = 0u, pw3 = 0u, pw4 = 0u;   /* words cw-1 .. cw-4 */
     uint32_t ms = 0u, me = 0u;         /* the last match: [ms, me) */
-    const uint8_t *const src_end = src + n;
+    uint32_t rel = 0u, q = 0u, k = 0u, lim = 0u, m = 0u;
+    bool ok = true;
+    uint32_t mode = n >= 3u ? K2_STEP : K2_DONE;
 
-#define LN_BYTE(pos, out_)                                                         \
+#define K2_PUT(bytes_, cnt_)                                                       \
     do {                                                                           \
-        const uint8_t *a_ = src + (pos);                                           \
-        const uint8_t *al_ = (const uint8_t *)((uintptr_t)a_ & ~(uintptr_t)15);   \
-        if (al_ != wa) {                                                           \
-            W = al_ == wa + 16 ? W2 : *(const uint4 *)al_;                         \
-            if (al_ + 16 < src_end) W2 = *(const uint4 *)(al_ + 16);               \
-            wa = al_;                                                              \
+        acc |= (uint64_t)(bytes_) << (8u * accn);                                  \
+        accn += (cnt_);                                                            \
+        if (accn >= 4u) {                                                          \
+            const uint32_t w_ = (uint32_t)acc;                                     \
+            uint8_t *a_ = da + 4u * fw;                                            \
+            if (fw != 0u || dm == 0u) {                                            \
+                *(uint32_t *)a_ = w_;                                              \
+            } else {                                                               \
+                for (uint32_t t_ = dm; t_ < 4u; t_++) a_[t_] = (uint8_t)(w_ >> (8u * t_)); \
+            }                                                                      \
+            fw++;                                                                  \
+            acc >>= 32;                                                            \
+            accn -= 4u;                                                            \
         }                                                                          \
-        const uint32_t o_ = (uint32_t)(a_ - al_);                                  \
-        (out_) = (ln_sel4(W, o_ >> 2) >> (8u * (o_ & 3u))) & 0xFFu;                \
+    } while (0)
+#define K2_PATCH(x_, byte_)                                                        \
+    do {                                                                           \
+        if ((x_) >= 4u * fw) {                                                     \
+            const uint32_t sh_ = 8u * ((x_) - 4u * fw);                            \
+            acc = (acc & ~(0xFFull << sh_)) | ((uint64_t)(byte_) << sh_);          \
+        } else {                                                                   \
+            da[(x_)] = (uint8_t)(byte_);                                           \
+        }                                                                          \
+    } while (0)
+#define K2_BYTE(pos_, out_)                                                        \
+    do {                                                                           \
+        const uint32_t x_ = sm + (pos_), b_ = x_ >> 4;                             \
+        if (b_ != wb) {                                                            \
+            W = b_ == wb + 1u ? W2 : *(const uint4 *)(sa + 16u * b_);              \
+            if (b_ < last_blk) W2 = *(const uint4 *)(sa + 16u * (b_ + 1u));        \
+            wb = b_;                                                               \
+        }                                                                          \
+        (out_) = (ln_sel4(W, (x_ >> 2) & 3u) >> (8u * (x_ & 3u))) & 0xFFu;        \
+    } while (0)
+#define K2_LITERAL(pos_)                                                           \
+    do {                                                                           \
+        uint32_t byte_;                                                            \
+        K2_BYTE(pos_, byte_);                                                      \
+        if (run == 0u) { hx = 4u * fw + accn; K2_PUT(byte_ << 8, 2u); }           \
+        else K2_PUT(byte_, 1u);                                                    \
+        o++;                                                                       \
+        if (++run == LZF_MAX_LIT) { K2_PATCH(hx, LZF_MAX_LIT - 1u); run = 0u; o++; } \
     } while (0)
 
-    while (n >= 3u && p < n - 2u) {                                   /* src/lzf_c.c:145 */
-        const uint32_t blk = p & ~7u;
-        if (blk != cb) {
-            C = blk == cb + 8u ? C2 : *(const uint4 *)(cand + blk);
-            C2 = *(const uint4 *)(cand + blk + 8u);                   /* scratch has slack */
-            cb = blk;
-        }
-        const uint32_t c = (ln_sel4(C, (p >> 1) & 3u) >> (16u * (p & 1u))) & 0xFFFFu;
-        /* rel: 0 no ref; 1 ref with other bytes; 2..6 equal for rel+1 bytes;
-         * 7 equal >= 8 bytes; 8 equal 3 bytes, length unknown; 9 unknown */
-        uint32_t rel = c >> 13;
-        uint32_t q = p - 1u - (c & 0x1FFFu);
-        if (rel) {
-            for (;;) {
-                bool ins;
-                if (q >= ms) {
-                    ins = !(q > ms && q + 3u <= me);                  /* interior of the last match */
-                } else {
-                    const uint32_t d = cw - (q >> 5);
-                    const uint32_t word = d == 0u ? curw : d == 1u ? pw1 : d == 2u ? pw2 :
-                                          d == 3u ? pw3 : d == 4u ? pw4 : bits[q >> 5];
-                    ins = (word >> (q & 31u)) & 1u;
+    while (__ballot(mode != K2_DONE)) {
+        /* ---- the cand word of p ------------------------------------------ */
+        if (mode == K2_STEP) {                                            /* src/lzf_c.c:145 */
+            if (p >= n - 2u) {
+                mode = K2_DONE;
+            } else {
+                const uint32_t blk = p & ~7u;
+                if (blk != cb) {
+                    C = blk == cb + 8u ? C2 : *(const uint4 *)(cand + blk);
+                    C2 = *(const uint4 *)(cand + blk + 8u);              /* scratch has slack */
+                    cb = blk;
                 }
-                if (ins) break;                                       /* q inserted: it is the ref */
+                const uint32_t c = (ln_sel4(C, (p >> 1) & 3u) >> (16u * (p & 1u))) & 0xFFFFu;
+                /* rel: 0 no ref; 1 ref with other bytes; 2..6 equal for rel+1
+                 * bytes; 7 equal >= 8; 8 equal 3 bytes, length unknown; 9 unknown */
+                rel = c >> 13;
+                q = p - 1u - (c & 0x1FFFu);
+                mode = rel ? K2_RESOLVE : K2_DECIDE;
+            }
+        }
+        /* ---- is the candidate inserted? else one link back --------------- */
+        if (mode == K2_RESOLVE) {
+            uint32_t word;
+            if (q >= ms) {
+                word = (q > ms && q + 3u <= me) ? 0u : 0xFFFFFFFFu;         /* last match's interior */
+            } else {
+                const uint32_t d = cw - (q >> 5);
+                word = d == 0u ? curw : d == 1u ? pw1 : d == 2u ? pw2 : d == 3u ? pw3 :
+                       d == 4u ? pw4 : bits[q >> 5];
+            }
+            if ((word >> (q & 31u)) & 1u) {                              /* q is the ref */
+                if (rel == 9u)
+                    rel = (src[q] == src[p] && src[q + 1u] == src[p + 1u] && src[q + 2u] == src[p + 2u]) ? 8u : 1u;
+                mode = K2_DECIDE;
+            } else {
                 const uint32_t c2 = cand[q];
                 const uint32_t r2 = c2 >> 13;
                 const uint32_t q2 = q - 1u - (c2 & 0x1FFFu);
-                if (!r2 || p - q2 - 1u >= LZF_WINDOW) { rel = 0u; break; }
-                const bool e1 = rel >= 2u && rel <= 8u, e2 = r2 >= 2u;
-                rel = rel == 9u ? 9u : (e1 && e2) ? 8u : (e1 != e2) ? 1u : 9u;
-                q = q2;
+                if (!r2 || p - q2 - 1u >= LZF_WINDOW) {
+                    rel = 0u;
+                    mode = K2_DECIDE;
+                } else {
+                    const bool e1 = rel >= 2u && rel <= 8u, e2 = r2 >= 2u;
+                    rel = rel == 9u ? 9u : (e1 && e2) ? 8u : (e1 != e2) ? 1u : 9u;
+                    q = q2;
+                }
             }
-            if (rel == 9u)
-                rel = (src[q] == src[p] && src[q + 1u] == src[p + 1u] && src[q + 2u] == src[p + 2u]) ? 8u : 1u;
         }
-        const bool hit = rel >= 2u && p + 4u < n;                    /* src/lzf_c.c:151-166 */
-        curw |= 1u << (p & 31u);                                     /* p is inserted */
-        if (!hit) {
-            if (o >= cap) { ok = false; break; }                     /* src/lzf_c.c:263 */
-            uint32_t byte;
-            LN_BYTE(p, byte);
-            if (run == 0u) { hp = E.wp(); E.put(byte << 8, 2u); }    /* header placeholder */
-            else E.put(byte, 1u);
-            o++;
-            if (++run == LZF_MAX_LIT) { E.patch(hp, LZF_MAX_LIT - 1u); run = 0u; o++; }
-            p++;
-            if ((p & 31u) == 0u) {
-                bits[cw] = curw;
-                pw4 = pw3; pw3 = pw2; pw2 = pw1; pw1 = curw;
-                cw++;
-                curw = 0u;
+        /* ---- literal, or the start of a back-reference ------------------- */
+        if (mode == K2_DECIDE) {
+            curw |= 1u << (p & 31u);                                     /* p is inserted */
+            if (!(rel >= 2u && p + 4u < n)) {                            /* src/lzf_c.c:151-166 */
+                if (o >= cap) {                                          /* src/lzf_c.c:263 */
+                    ok = false;
+                    mode = K2_DONE;
+                } else {
+                    K2_LITERAL(p);
+                    p++;
+                    if ((p & 31u) == 0u) {
+                        bits[cw] = curw;
+                        pw4 = pw3; pw3 = pw2; pw2 = pw1; pw1 = curw;
+                        cw++;
+                        curw = 0u;
+                    }
+                    mode = K2_STEP;
+                }
+            } else {
+                uint32_t maxlen = n - p - 2u;                            /* src/lzf_c.c:169-170 */
+                if (maxlen > LZF_MAX_REF) maxlen = LZF_MAX_REF;
+                lim = (maxlen > 16u && maxlen < 19u) ? 19u : maxlen;
+                if (rel <= 6u) {
+                    m = rel + 1u < lim ? rel + 1u : lim;
+                    mode = K2_EMIT;
+                } else {
+                    k = rel == 7u ? 8u : 3u;
+                    mode = K2_EXTEND;
+                }
             }
-            continue;
         }
-        uint32_t maxlen = n - p - 2u;                                /* src/lzf_c.c:169-170 */
-        if (maxlen > LZF_MAX_REF) maxlen = LZF_MAX_REF;
-        const uint32_t lim = (maxlen > 16u && maxlen < 19u) ? 19u : maxlen;
-        uint32_t m;
-        if (rel <= 6u) {
-            m = rel + 1u;
-            if (m > lim) m = lim;
-        } else {
-            m = ln_extend(src, n, p, q, rel == 7u ? 8u : 3u, lim);
+        /* ---- one 16-byte piece of a long match --------------------------- */
+        if (mode == K2_EXTEND) {
+            if (k < lim) {
+                const uint32_t avail = n - (p + k);
+                const uint4 a = ln_ld16_safe(src + p + k, avail), b = ln_ld16_safe(src + q + k, avail);
+                const uint32_t d = ln_first_diff(a, b);
+                k += d;
+                if (d < 16u) lim = k < lim ? k : lim;
+            }
+            if (k >= lim) {
+                m = lim;
+                mode = K2_EMIT;
+            }
         }
-        const uint32_t off = p - q - 1u;
-        if (run) E.patch(hp, run - 1u);                              /* close the run */
-        else o--;                                                    /* undo empty run */
-        if (o + 4u >= cap) { ok = false; break; }                    /* src/lzf_c.c:176 */
-        const uint32_t L = m - 2u;
-        if (L < 7u) {
-            E.put(((off >> 8) | (L << 5)) | ((off & 0xFFu) << 8), 2u);
-            o += 2u;
-        } else {
-            E.put((0xE0u | (off >> 8)) | ((L - 7u) << 8) | ((off & 0xFFu) << 16), 3u);
-            o += 3u;
-        }
-        run = 0u;
-        o++;                                                         /* reserve a header */
-        ms = p;
-        p += m;
-        me = p;
-        if (p >= n - 2u) break;                                      /* src/lzf_c.c:229 */
-        /* the two last positions of the match are inserted, its interior not */
-        const uint32_t nw = p >> 5, t1 = p - 2u, t2 = p - 1u;
-        const uint32_t b1 = 1u << (t1 & 31u), b2 = 1u << (t2 & 31u);
-        if (nw == cw) {
-            curw |= b1 | b2;
-        } else {
-            uint32_t wo = curw, wm = 0u, wn = 0u;
-            if ((t1 >> 5) == cw) wo |= b1; else if ((t1 >> 5) == nw) wn |= b1; else wm |= b1;
-            if ((t2 >> 5) == cw) wo |= b2; else if ((t2 >> 5) == nw) wn |= b2; else wm |= b2;
-            bits[cw] = wo;
-            if (wm) bits[nw - 1u] = wm;
-            const uint32_t d = nw - cw;          /* words cw+1 .. nw-2 stay all-interior (0) */
-            const uint32_t n1 = d == 1u ? wo : wm;
-            const uint32_t n2 = d == 1u ? pw1 : d == 2u ? wo : 0u;
-            const uint32_t n3 = d == 1u ? pw2 : d == 2u ? pw1 : d == 3u ? wo : 0u;
-            const uint32_t n4 = d == 1u ? pw3 : d == 2u ? pw2 : d == 3u ? pw1 : d == 4u ? wo : 0u;
-            pw1 = n1; pw2 = n2; pw3 = n3; pw4 = n4;
-            curw = wn;
-            cw = nw;
+        /* ---- the back-reference ------------------------------------------ */
+        if (mode == K2_EMIT) {
+            const uint32_t off = p - q - 1u;
+            if (run) K2_PATCH(hx, run - 1u);                             /* close the run */
+            else o--;                                                    /* undo empty run */
+            if (o + 4u >= cap) {                                         /* src/lzf_c.c:176 */
+                ok = false;
+                mode = K2_DONE;
+            } else {
+                const uint32_t L = m - 2u;
+                if (L < 7u) {
+                    K2_PUT(((off >> 8) | (L << 5)) | ((off & 0xFFu) << 8), 2u);
+                    o += 2u;
+                } else {
+                    K2_PUT((0xE0u | (off >> 8)) | ((L - 7u) << 8) | ((off & 0xFFu) << 16), 3u);
+                    o += 3u;
+                }
+                run = 0u;
+                o++;                                                     /* reserve a header */
+                ms = p;
+                p += m;
+                me = p;
+                if (p >= n - 2u) {                                       /* src/lzf_c.c:229 */
+                    mode = K2_DONE;
+                } else {
+                    /* the two last positions of the match are inserted, its interior not */
+                    const uint32_t nw = p >> 5, t1 = p - 2u, t2 = p - 1u;
+                    const uint32_t b1 = 1u << (t1 & 31u), b2 = 1u << (t2 & 31u);
+                    if (nw == cw) {
+                        curw |= b1 | b2;
+                    } else {
+                        uint32_t wo = curw, wm = 0u, wn = 0u;
+                        if ((t1 >> 5) == cw) wo |= b1; else if ((t1 >> 5) == nw) wn |= b1; else wm |= b1;
+                        if ((t2 >> 5) == cw) wo |= b2; else if ((t2 >> 5) == nw) wn |= b2; else wm |= b2;
+                        bits[cw] = wo;
+                        if (wm) bits[nw - 1u] = wm;
+                        const uint32_t d = nw - cw;      /* words cw+1 .. nw-2 stay all-interior (0) */
+                        const uint32_t n1 = d == 1u ? wo : wm;
+                        const uint32_t n2 = d == 1u ? pw1 : d == 2u ? wo : 0u;
+                        const uint32_t n3 = d == 1u ? pw2 : d == 2u ? pw1 : d == 3u ? wo : 0u;
+                        const uint32_t n4 = d == 1u ? pw3 : d == 2u ? pw2 : d == 3u ? pw1 : d == 4u ? wo : 0u;
+                        pw1 = n1; pw2 = n2; pw3 = n3; pw4 = n4;
+                        curw = wn;
+                        cw = nw;
+                    }
+                    mode = K2_STEP;
+                }
+            }
         }
     }
     if (!ok || o + 3u > cap) { bt.out_len[v] = 0u; return; }          /* src/lzf_c.c:276 */
     while (p < n) {                                                   /* src/lzf_c.c:279-288 */
-        uint32_t byte;
-        LN_BYTE(p, byte);
-        if (run == 0u) { hp = E.wp(); E.put(byte << 8, 2u); }
-        else E.put(byte, 1u);
-        o++;
-        if (++run == LZF_MAX_LIT) { E.patch(hp, LZF_MAX_LIT - 1u); run = 0u; o++; }
+        K2_LITERAL(p);
         p++;
     }
-#undef LN_BYTE
-    if (run) E.patch(hp, run - 1u);
+    if (run) K2_PATCH(hx, run - 1u);
     else o--;
-    E.finish();
+    for (uint32_t t = 0; t < accn; t++)
+        if (4u * fw + t >= dm) da[4u * fw + t] = (uint8_t)(acc >> (8u * t));
     bt.out_len[v] = o;
+#undef K2_PUT
+#undef K2_PATCH
+#undef K2_BYTE
+#undef K2_LITERAL
 }
 
 /* ---- launcher ------------------------------------------------------------ */

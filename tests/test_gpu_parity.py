@@ -84,6 +84,19 @@ def test_batch_compress_golden(golden, generation):
     assert not bad, f"{len(bad)} mismatches, first: {bad[:5]}"
 
 
+@pytest.mark.parametrize("nmax", [4096, 65536])
+def test_batch_compress_golden_by_size(golden, generation, nmax):
+    # batches whose largest value selects each kernel class of a generation
+    # (a batch with any value past 64 KiB runs the window generation)
+    from tests.gpu_batch import gpu_compress
+    cases = [c for c in golden["compress"] if c["n"] <= min(nmax, _limit(generation))]
+    vals = [synth(c["kind"], c["seed"], c["index"], c["n"]) for c in cases]
+    res = gpu_compress(vals, [c["out_len"] for c in cases])
+    bad = [(c["kind"], c["n"], c["out_len"]) for c, r in zip(cases, res)
+           if (len(r) if r else 0) != c["result"] or (r and sha16(r) != c["out_sha"])]
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:5]}"
+
+
 def test_batch_decompress_golden(golden, oracle):
     from tests.gpu_batch import gpu_decompress
     from tests.test_oracle import decoder_cases
