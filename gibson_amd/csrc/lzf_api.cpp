@@ -77,6 +77,8 @@ struct Scratch {
     hipEvent_t ev = nullptr;
     hipStream_t last = nullptr;
     bool used = false;
+    hipStream_t aux = nullptr;      /* kernel-2 stream of the chunk pipeline */
+    hipEvent_t pev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 size_t scratch_limit()
@@ -98,7 +100,7 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s)
     size_t want = per * (size_t)b.count + 512;
     const size_t lim = scratch_limit();
     if (want > lim) want = lim;
-    if (want < per + 512) want = per + 512;
+    if (want < 2 * per + 1024) want = 2 * per + 1024;     /* two pipeline halves */
     if (S.cap < want) {
         if (S.p) {
             (void)hipDeviceSynchronize();
@@ -114,7 +116,15 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s)
     if (!S.ev && (e = hipEventCreateWithFlags(&S.ev, hipEventDisableTiming)) != hipSuccess) return e;
     if (S.used && S.last != s && (e = hipStreamWaitEvent(s, S.ev, 0)) != hipSuccess) return e;
     const char *ff = getenv("LZF_GPU_LANE_FORCE_FIX");
-    e = lzf_launch_compress_lane(b, s, S.p, S.cap, (ff && *ff == '1') ? 1u : 0u);
+    const char *pp = getenv("LZF_GPU_LANE_PIPE");
+    const bool pipe = !(pp && *pp == '0');
+    if (pipe && !S.aux) {
+        if ((e = hipStreamCreateWithFlags(&S.aux, hipStreamNonBlocking)) != hipSuccess) return e;
+        for (int k = 0; k < 4; k++)
+            if ((e = hipEventCreateWithFlags(&S.pev[k], hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    e = lzf_launch_compress_lane(b, s, S.p, S.cap, (ff && *ff == '1') ? 1u : 0u,
+                                 pipe ? S.aux : nullptr, pipe ? S.pev : nullptr);
     if (e != hipSuccess) return e;
     e = hipEventRecord(S.ev, s);
     S.last = s;
@@ -133,12 +143,22 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
     }
 }
 
+/* The lane decoder (one lane per stream) is bit-exact but, streaming 64
+ * values per wave through L2, slower than tokpar64 on the BASELINE shapes
+ * (DESIGN.md §4.3); the lane generation therefore decodes with tokpar64
+ * unless LZF_GPU_DECOMPRESS=lane asks for the lane decoder. */
+bool lane_decoder()
+{
+    const char *e = getenv("LZF_GPU_DECOMPRESS");
+    return e && !strcmp(e, "lane");
+}
+
 hipError_t launch_decompress(const LzfBatch &b, hipStream_t s)
 {
     switch (kernel_gen()) {
     case GEN_SERIAL: return lzf_launch_decompress_serial(b, s);
     case GEN_WINDOW: return lzf_launch_decompress(b, s);
-    default: return lzf_launch_decompress_lane(b, s);
+    default: return lane_decoder() ? lzf_launch_decompress_lane(b, s) : lzf_launch_decompress(b, s);
     }
 }
 
@@ -417,7 +437,10 @@ const char *lzf_gpu_kernel_info(void)
         s = std::string("compress=") + lzf_compress_kernel_name() + " decompress=" +
             lzf_decompress_kernel_name();
         break;
-    default: s = "compress=lane(cand+parse; window64 past 64 KiB) decompress=lane"; break;
+    default:
+        s = std::string("compress=lane(cand+parse; window64 past 64 KiB) decompress=") +
+            (lane_decoder() ? "lane" : lzf_decompress_kernel_name());
+        break;
     }
     return s.c_str();
 }

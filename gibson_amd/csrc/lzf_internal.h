@@ -65,8 +65,11 @@ struct LzfLaneScratch {
 
 /* launchers, defined next to their kernels; return hipSuccess or the error */
 hipError_t lzf_launch_decompress_lane(const LzfBatch &b, hipStream_t s);
+/* aux / ev (4 events) optional: chunks pipelined over s (kernel 1) and aux
+ * (kernel 2); s is joined with aux before returning */
 hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scratch,
-                                    size_t scratch_bytes, uint32_t force_fix);
+                                    size_t scratch_bytes, uint32_t force_fix, hipStream_t aux,
+                                    hipEvent_t *ev);
 size_t lzf_lane_scratch_per_value(uint32_t max_len);
 bool lzf_lane_compress_supported(uint32_t max_len);
 hipError_t lzf_launch_compress(const LzfBatch &b, hipStream_t s);

@@ -31,6 +31,8 @@
  *
  * Scratch per value: 2 B/position (cand) + 1 bit/position (bitmap).
  */
+#include <stdlib.h>
+
 #include "lzf_internal.h"
 
 /* ---- small helpers ------------------------------------------------------ */
@@ -229,10 +231,31 @@ __global__ __launch_bounds__(LD_THREADS) void lzf_decompress_lane_kernel(LzfBatc
     bt.err[v] = err;
 }
 
+/* Residency cap for the one-lane-per-value kernels: each lane streams its own
+ * value, so the lines in use grow with the lanes in flight; past what the
+ * XCD's L2 holds every access refetches its line.  Capping the blocks per CU
+ * (through the LDS reservation of the launch) trades latency hiding for
+ * L2 hits.  0 = no cap. */
+static size_t lane_lds_for(const char *env, uint32_t dflt_blocks_per_cu)
+{
+    const char *e = getenv(env);
+    const uint32_t b = e ? (uint32_t)atoi(e) : dflt_blocks_per_cu;
+    if (b == 0u) return 0;
+    size_t lds = (160u * 1024u) / b;
+    if (lds > 64u * 1024u) lds = 64u * 1024u;
+    return lds - 256u;
+}
+
 hipError_t lzf_launch_decompress_lane(const LzfBatch &b, hipStream_t s)
 {
     const uint32_t grid = (b.count + LD_THREADS - 1u) / LD_THREADS;
-    hipLaunchKernelGGL(lzf_decompress_lane_kernel, dim3(grid), dim3(LD_THREADS), 0, s, b);
+    const size_t lds = lane_lds_for("LZF_LANE_DEC_BLOCKS", 0u);
+    if (lds) {
+        hipError_t e = hipFuncSetAttribute((const void *)lzf_decompress_lane_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(lzf_decompress_lane_kernel, dim3(grid), dim3(LD_THREADS), lds, s, b);
     return hipGetLastError();
 }
 
@@ -250,6 +273,9 @@ hipError_t lzf_launch_decompress_lane(const LzfBatch &b, hipStream_t s)
 #define CAND_LONG   7u
 
 #define K1_WIN      4u            /* windows of 64 positions resolved per step */
+#ifndef KS_WIN
+#define KS_WIN      4u            /* small class: windows per step */
+#endif
 #define KS_BUCKETS  4096u         /* small class: 12-bit bucket, 4-bit identity */
 #define KS_MAXN     4096u         /* staged whole; positions + 1 fit 12 bits */
 #define KM_BUCKETS  2048u         /* mid class */
@@ -357,12 +383,12 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
     __shared__ __attribute__((aligned(16))) uint16_t H[KS_BUCKETS];
     __shared__ uint16_t E[KS_MAXN];
     __shared__ __attribute__((aligned(16))) uint32_t Bw[KS_MAXN / 4u + 4u];
-    __shared__ unsigned long long T[K1_WIN][KS_TN];
+    __shared__ unsigned long long T[KS_WIN][KS_TN];
     const uint32_t lane = threadIdx.x;
     const unsigned long long mine = 1ull << lane, below = mine - 1ull;
     uint32_t v = blockIdx.x;
     if (v >= bt.count) return;
-    for (uint32_t k = lane; k < K1_WIN * KS_TN; k += 64u) (&T[0][0])[k] = 0ull;
+    for (uint32_t k = lane; k < KS_WIN * KS_TN; k += 64u) (&T[0][0])[k] = 0ull;
     uint4 pf[4];
     uint32_t pn = bt.in_len[v];
     {
@@ -394,11 +420,11 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
             for (uint32_t k = lane; k < KS_BUCKETS / 8u; k += 64u) ((uint4 *)H)[k] = make_uint4(0, 0, 0, 0);
             ln_wave_fence();
             const uint32_t np = n - 2u;               /* positions 0 .. n-3 */
-            for (uint32_t P = 0; P < np; P += 64u * K1_WIN) {
-                uint32_t p[K1_WIN], m[K1_WIN], tri[K1_WIN];
-                bool act[K1_WIN];
+            for (uint32_t P = 0; P < np; P += 64u * KS_WIN) {
+                uint32_t p[KS_WIN], m[KS_WIN], tri[KS_WIN];
+                bool act[KS_WIN];
 #pragma unroll
-                for (uint32_t j = 0; j < K1_WIN; j++) {
+                for (uint32_t j = 0; j < KS_WIN; j++) {
                     p[j] = P + 64u * j + lane;
                     act[j] = p[j] < np;
                     tri[j] = ks_rd4(Bw, act[j] ? p[j] : 0u);
@@ -410,16 +436,16 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                     }
                 }
                 ln_wave_fence();
-                unsigned long long MB[K1_WIN], MS[K1_WIN];
+                unsigned long long MB[KS_WIN], MS[KS_WIN];
 #pragma unroll
-                for (uint32_t j = 0; j < K1_WIN; j++) {
+                for (uint32_t j = 0; j < KS_WIN; j++) {
                     MB[j] = T[j][KS_T0 + ((m[j] >> 4) & 63u)] & T[j][KS_T1 + (m[j] >> 10)];
                     MS[j] = MB[j] & T[j][KS_T2 + (m[j] & 15u)];
                     if (!act[j]) MB[j] = MS[j] = 0ull;
                 }
                 ln_wave_fence();
 #pragma unroll
-                for (uint32_t j = 0; j < K1_WIN; j++) {
+                for (uint32_t j = 0; j < KS_WIN; j++) {
                     if (act[j]) {
                         T[j][KS_T0 + ((m[j] >> 4) & 63u)] = 0ull;
                         T[j][KS_T1 + (m[j] >> 10)] = 0ull;
@@ -428,10 +454,10 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                 }
                 /* window j reads the heads after window j-1 wrote them (LDS
                  * ops of a wave execute in order) */
-                uint32_t q1[K1_WIN], cur[K1_WIN];
+                uint32_t q1[KS_WIN], cur[KS_WIN];
                 bool need = false;
 #pragma unroll
-                for (uint32_t j = 0; j < K1_WIN; j++) {
+                for (uint32_t j = 0; j < KS_WIN; j++) {
                     const uint32_t bk = m[j] >> 4, id = m[j] & 15u;
                     const uint32_t key = ((p[j] + 1u) << 4) | id;
                     const unsigned long long ss = MS[j] & below, sb = MB[j] & ~MS[j] & below;
@@ -453,7 +479,7 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                 while (__ballot(need)) {
                     need = false;
 #pragma unroll
-                    for (uint32_t j = 0; j < K1_WIN; j++) {
+                    for (uint32_t j = 0; j < KS_WIN; j++) {
                         if (cur[j]) {
                             const uint32_t e = E[(cur[j] >> 4) - 1u];
                             cur[j] = e;
@@ -463,7 +489,7 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                     }
                 }
 #pragma unroll
-                for (uint32_t j = 0; j < K1_WIN; j++) {
+                for (uint32_t j = 0; j < KS_WIN; j++) {
                     if (!act[j]) continue;
                     uint32_t w = 0u;
                     if (q1[j] > 1u) {                    /* q = q1 - 1 > 0 */
@@ -840,20 +866,33 @@ size_t lzf_lane_scratch_per_value(uint32_t max_len)
 bool lzf_lane_compress_supported(uint32_t max_len) { return max_len <= KM_MAXN; }
 
 hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scratch,
-                                    size_t scratch_bytes, uint32_t force_fix)
+                                    size_t scratch_bytes, uint32_t force_fix, hipStream_t aux,
+                                    hipEvent_t *ev)
 {
     if (b.max_len > KM_MAXN) return hipErrorInvalidValue;
     const uint64_t cstride = lane_cstride(b.max_len), bstride = lane_bstride(b.max_len);
-    uint64_t chunk = scratch_bytes / lzf_lane_scratch_per_value(b.max_len);
+    /* with an aux stream: two scratch halves, kernel 1 of chunk i+1 on s
+     * overlaps kernel 2 of chunk i on aux */
+    const bool pipe = aux != nullptr && ev != nullptr &&
+                      scratch_bytes / 2u >= lzf_lane_scratch_per_value(b.max_len) + 512u && b.count >= 4u;
+    const size_t half = pipe ? (scratch_bytes / 2u) & ~(size_t)255 : scratch_bytes;
+    uint64_t chunk = half / lzf_lane_scratch_per_value(b.max_len);
     const auto bits_at = [&](uint64_t ch) { return ((ch * cstride * 2u) + 255u) & ~255ull; };
-    while (chunk && bits_at(chunk) + chunk * bstride * 4u > scratch_bytes) chunk--;
+    while (chunk && bits_at(chunk) + chunk * bstride * 4u > half) chunk--;
     if (chunk == 0) return hipErrorInvalidValue;
-    LzfLaneScratch sc;
-    sc.cand = (uint16_t *)scratch;
-    sc.bits = (uint32_t *)((uint8_t *)scratch + bits_at(chunk));
-    sc.cstride = cstride;
-    sc.bstride = bstride;
-    sc.force_fix = force_fix;
+    if (pipe) {                       /* at least 4 chunks so the stages overlap */
+        const uint64_t quarter = (b.count + 3u) / 4u;
+        if (quarter < chunk) chunk = quarter < 1024u ? (b.count < 1024u ? b.count : 1024u) : quarter;
+    }
+    LzfLaneScratch sc[2];
+    for (int h = 0; h < 2; h++) {
+        uint8_t *base = (uint8_t *)scratch + (pipe ? h * half : 0);
+        sc[h].cand = (uint16_t *)base;
+        sc[h].bits = (uint32_t *)(base + bits_at(chunk));
+        sc[h].cstride = cstride;
+        sc[h].bstride = bstride;
+        sc[h].force_fix = force_fix;
+    }
     /* the small-class kernel is persistent: as many one-wave workgroups as
      * stay resident (LDS-bound), each walking the batch */
     uint32_t small_grid = 256u * 8u;
@@ -870,8 +909,17 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
             small_grid = (uint32_t)cus * per;
         }
     }
-    for (uint64_t first = 0; first < b.count; first += chunk) {
+    const size_t parse_lds = lane_lds_for("LZF_LANE_PARSE_BLOCKS", 0u);
+    if (parse_lds) {
+        hipError_t e = hipFuncSetAttribute((const void *)lzf_parse_lane_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)parse_lds);
+        if (e != hipSuccess) return e;
+    }
+    hipError_t e;
+    uint32_t i = 0;
+    for (uint64_t first = 0; first < b.count; first += chunk, i++) {
         const uint32_t cnt = (uint32_t)((b.count - first) < chunk ? (b.count - first) : chunk);
+        const int h = pipe ? (int)(i & 1u) : 0;
         LzfBatch c = b;
         c.in_off = b.in_off + first;
         c.in_len = b.in_len + first;
@@ -879,18 +927,29 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
         c.out_cap = b.out_cap + first;
         c.out_len = b.out_len + first;
         c.count = cnt;
+        /* scratch half h is free once kernel 2 of chunk i-2 is done */
+        if (pipe && i >= 2u && (e = hipStreamWaitEvent(s, ev[2 + h], 0)) != hipSuccess) return e;
         if (b.max_len <= KS_MAXN) {
             const uint32_t g = cnt < small_grid ? cnt : small_grid;
-            hipLaunchKernelGGL(lzf_cand_small_kernel, dim3(g), dim3(64), 0, s, c, sc);
+            hipLaunchKernelGGL(lzf_cand_small_kernel, dim3(g), dim3(64), 0, s, c, sc[h]);
+        } else {
+            hipLaunchKernelGGL(lzf_cand_mid_kernel, dim3(cnt), dim3(64), 0, s, c, sc[h]);
         }
-        else
-            hipLaunchKernelGGL(lzf_cand_mid_kernel, dim3(cnt), dim3(64), 0, s, c, sc);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipStream_t s2 = s;
+        if (pipe) {
+            if ((e = hipEventRecord(ev[h], s)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(aux, ev[h], 0)) != hipSuccess) return e;
+            s2 = aux;
+        }
         hipLaunchKernelGGL(lzf_parse_lane_kernel, dim3((cnt + K2_THREADS - 1u) / K2_THREADS),
-                           dim3(K2_THREADS), 0, s, c, sc);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
+                           dim3(K2_THREADS), parse_lds, s2, c, sc[h]);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (pipe && (e = hipEventRecord(ev[2 + h], aux)) != hipSuccess) return e;
+    }
+    if (pipe) {                       /* join: s waits for the last kernel 2 of both halves */
+        for (uint32_t h = 0; h < 2u && h < i; h++)
+            if ((e = hipStreamWaitEvent(s, ev[2 + h], 0)) != hipSuccess) return e;
     }
     return hipSuccess;
 }

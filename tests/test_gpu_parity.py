@@ -111,10 +111,30 @@ def test_batch_decompress_golden(golden, oracle):
     assert not bad, f"{len(bad)} mismatches, first: {bad[:5]}"
 
 
-@pytest.mark.parametrize("gen", ["window", "serial"])
+@pytest.mark.parametrize("gen", ["window", "serial", "lane-decoder"])
 def test_batch_decompress_other_generations(golden, oracle, monkeypatch, gen):
-    monkeypatch.setenv("LZF_GPU_KERNEL", gen)
+    if gen == "lane-decoder":
+        monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+        monkeypatch.setenv("LZF_GPU_DECOMPRESS", "lane")
+    else:
+        monkeypatch.setenv("LZF_GPU_KERNEL", gen)
     test_batch_decompress_golden(golden, oracle)
+
+
+def test_lane_decoder_edge_and_unaligned(oracle, monkeypatch):
+    from tests.gpu_batch import gpu_decompress
+    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.setenv("LZF_GPU_DECOMPRESS", "lane")
+    streams = [b"", b"\x00", b"\xe0\x00\x00", b"\x1f" + b"q" * 31, b"\x00z\xa0\x00"]
+    for cap in (0, 1, 7, 8, 32, 4096):
+        dec = gpu_decompress(streams, [cap] * len(streams), align=3)
+        for s_, d in zip(streams, dec):
+            assert d == oracle.decompress(s_, cap), (s_, cap)
+    rnd = random.Random(9)
+    vals = [synth(rnd.randrange(6), 0x5EED00E0, i, rnd.randint(1, 9000)) for i in range(500)]
+    streams = [oracle.compress(v, len(v) + len(v) // 16 + 64) for v in vals]
+    assert all(streams)
+    assert gpu_decompress(streams, [len(v) for v in vals], align=1) == [(v, 0) for v in vals]
 
 
 @pytest.mark.parametrize("align", [1, 3])
