@@ -116,8 +116,11 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s)
     if (!S.ev && (e = hipEventCreateWithFlags(&S.ev, hipEventDisableTiming)) != hipSuccess) return e;
     if (S.used && S.last != s && (e = hipStreamWaitEvent(s, S.ev, 0)) != hipSuccess) return e;
     const char *ff = getenv("LZF_GPU_LANE_FORCE_FIX");
+    /* LZF_GPU_LANE_PIPE=1 overlaps the two kernels of consecutive chunks on
+     * two streams; off by default: both kernels hold LDS and do not co-reside
+     * well */
     const char *pp = getenv("LZF_GPU_LANE_PIPE");
-    const bool pipe = !(pp && *pp == '0');
+    const bool pipe = pp && *pp == '1';
     if (pipe && !S.aux) {
         if ((e = hipStreamCreateWithFlags(&S.aux, hipStreamNonBlocking)) != hipSuccess) return e;
         for (int k = 0; k < 4; k++)

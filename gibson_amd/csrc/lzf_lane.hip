@@ -602,6 +602,27 @@ __global__ __launch_bounds__(64) void lzf_cand_mid_kernel(LzfBatch bt, LzfLaneSc
 /* ======================================================================== */
 
 #define K2_THREADS 256u
+#ifndef K2_RW
+#define K2_RW      32u          /* bitmap words kept in LDS per lane (power of two) */
+#endif
+
+/* Diagnostic build only (-DK2_COUNT_SITES): per-site event counts of the
+ * parse kernel's global memory accesses, summed over all lanes. */
+#ifdef K2_COUNT_SITES
+__device__ unsigned long long k2_sites[16];
+#define K2_SITE(i) atomicAdd(&k2_sites[i], 1ull)
+extern "C" int lzf_gpu_debug_sites(unsigned long long *out16, int reset)
+{
+    hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(k2_sites), sizeof(k2_sites));
+    if (e == hipSuccess && reset) {
+        unsigned long long z[16] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(k2_sites), z, sizeof(z));
+    }
+    return e == hipSuccess ? 0 : -2;
+}
+#else
+#define K2_SITE(i) ((void)0)
+#endif
 
 /* m = min(first mismatch >= start, lim), bytes [0, start) known equal
  * (src/lzf_c.c:169-209; lim carries the 16-compare quirk) */
@@ -642,7 +663,11 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
     uint32_t cb = 0xFFFFFFF0u;         /* cand entries [cb, cb+8) (+ next 8); none yet */
     uint4 C = W, C2 = W;
     uint32_t cw = 0u, curw = 0u;       /* inserted-bitmap word of p, in flight */
-    uint32_t pw1 = 0u, pw2 = 0u, pw3 = 0u, pw4 = 0u;   /* words cw-1 .. cw-4 */
+    /* the last K2_RW bitmap words of the value in LDS (word w at slot w % K2_RW,
+     * lane-interleaved: conflict-free), older words in the scratch array */
+    __shared__ uint32_t k2_ring[K2_RW][K2_THREADS];
+    uint32_t *const ring = &k2_ring[0][threadIdx.x];
+#define K2_RING(w_) ring[((w_) & (K2_RW - 1u)) * K2_THREADS]
     uint32_t ms = 0u, me = 0u;         /* the last match: [ms, me) */
     uint32_t rel = 0u, q = 0u, k = 0u, lim = 0u, m = 0u;
     bool ok = true;
@@ -660,6 +685,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
             } else {                                                               \
                 for (uint32_t t_ = dm; t_ < 4u; t_++) a_[t_] = (uint8_t)(w_ >> (8u * t_)); \
             }                                                                      \
+            K2_SITE(8);                                                            \
             fw++;                                                                  \
             acc >>= 32;                                                            \
             accn -= 4u;                                                            \
@@ -678,6 +704,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
     do {                                                                           \
         const uint32_t x_ = sm + (pos_), b_ = x_ >> 4;                             \
         if (b_ != wb) {                                                            \
+            K2_SITE(6);                                                            \
             W = b_ == wb + 1u ? W2 : *(const uint4 *)(sa + 16u * b_);              \
             if (b_ < last_blk) W2 = *(const uint4 *)(sa + 16u * (b_ + 1u));        \
             wb = b_;                                                               \
@@ -695,13 +722,16 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
     } while (0)
 
     while (__ballot(mode != K2_DONE)) {
+        if (mode != K2_DONE) K2_SITE(0);
         /* ---- the cand word of p ------------------------------------------ */
         if (mode == K2_STEP) {                                            /* src/lzf_c.c:145 */
             if (p >= n - 2u) {
                 mode = K2_DONE;
             } else {
                 const uint32_t blk = p & ~7u;
+                K2_SITE(10);
                 if (blk != cb) {
+                    if (blk == cb + 8u) K2_SITE(2); else K2_SITE(1);
                     C = blk == cb + 8u ? C2 : *(const uint4 *)(cand + blk);
                     C2 = *(const uint4 *)(cand + blk + 8u);              /* scratch has slack */
                     cb = blk;
@@ -721,14 +751,16 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                 word = (q > ms && q + 3u <= me) ? 0u : 0xFFFFFFFFu;         /* last match's interior */
             } else {
                 const uint32_t d = cw - (q >> 5);
-                word = d == 0u ? curw : d == 1u ? pw1 : d == 2u ? pw2 : d == 3u ? pw3 :
-                       d == 4u ? pw4 : bits[q >> 5];
+                if (d >= K2_RW) K2_SITE(3);
+                word = d == 0u ? curw : d < K2_RW ? K2_RING(q >> 5) : bits[q >> 5];
             }
             if ((word >> (q & 31u)) & 1u) {                              /* q is the ref */
+                if (rel == 9u) K2_SITE(5);
                 if (rel == 9u)
                     rel = (src[q] == src[p] && src[q + 1u] == src[p + 1u] && src[q + 2u] == src[p + 2u]) ? 8u : 1u;
                 mode = K2_DECIDE;
             } else {
+                K2_SITE(4);
                 const uint32_t c2 = cand[q];
                 const uint32_t r2 = c2 >> 13;
                 const uint32_t q2 = q - 1u - (c2 & 0x1FFFu);
@@ -754,7 +786,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                     p++;
                     if ((p & 31u) == 0u) {
                         bits[cw] = curw;
-                        pw4 = pw3; pw3 = pw2; pw2 = pw1; pw1 = curw;
+                        K2_RING(cw) = curw;
                         cw++;
                         curw = 0u;
                     }
@@ -776,6 +808,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
         /* ---- one 16-byte piece of a long match --------------------------- */
         if (mode == K2_EXTEND) {
             if (k < lim) {
+                K2_SITE(7);
                 const uint32_t avail = n - (p + k);
                 const uint4 a = ln_ld16_safe(src + p + k, avail), b = ln_ld16_safe(src + q + k, avail);
                 const uint32_t d = ln_first_diff(a, b);
@@ -823,12 +856,9 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                         if ((t2 >> 5) == cw) wo |= b2; else if ((t2 >> 5) == nw) wn |= b2; else wm |= b2;
                         bits[cw] = wo;
                         if (wm) bits[nw - 1u] = wm;
-                        const uint32_t d = nw - cw;      /* words cw+1 .. nw-2 stay all-interior (0) */
-                        const uint32_t n1 = d == 1u ? wo : wm;
-                        const uint32_t n2 = d == 1u ? pw1 : d == 2u ? wo : 0u;
-                        const uint32_t n3 = d == 1u ? pw2 : d == 2u ? pw1 : d == 3u ? wo : 0u;
-                        const uint32_t n4 = d == 1u ? pw3 : d == 2u ? pw2 : d == 3u ? pw1 : d == 4u ? wo : 0u;
-                        pw1 = n1; pw2 = n2; pw3 = n3; pw4 = n4;
+                        K2_RING(cw) = wo;
+                        /* words cw+1 .. nw-2 are all interior (0), nw-1 holds tails */
+                        for (uint32_t w = cw + 1u; w < nw; w++) K2_RING(w) = w + 1u == nw ? wm : 0u;
                         curw = wn;
                         cw = nw;
                     }
@@ -851,6 +881,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
 #undef K2_PATCH
 #undef K2_BYTE
 #undef K2_LITERAL
+#undef K2_RING
 }
 
 /* ---- launcher ------------------------------------------------------------ */
