@@ -141,7 +141,7 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
     case GEN_SERIAL: return lzf_launch_compress_serial(b, s);
     case GEN_WINDOW: return lzf_launch_compress(b, s);
     default:
-        /* values past 64 KiB go to the window generation (64-bit heads) */
+        /* batches with values past 4 KiB go to the window generation */
         return lzf_lane_compress_supported(b.max_len) ? lane_compress(b, s) : lzf_launch_compress(b, s);
     }
 }
@@ -441,7 +441,7 @@ const char *lzf_gpu_kernel_info(void)
             lzf_decompress_kernel_name();
         break;
     default:
-        s = std::string("compress=lane(cand+parse; window64 past 64 KiB) decompress=") +
+        s = std::string("compress=lane(cand+parse; window64 past 4 KiB) decompress=") +
             (lane_decoder() ? "lane" : lzf_decompress_kernel_name());
         break;
     }

@@ -894,7 +894,15 @@ size_t lzf_lane_scratch_per_value(uint32_t max_len)
     return (size_t)(lane_cstride(max_len) * 2u + lane_bstride(max_len) * 4u);
 }
 
-bool lzf_lane_compress_supported(uint32_t max_len) { return max_len <= KM_MAXN; }
+/* The default lane path takes the small class only: on longer values the
+ * window generation is faster today; LZF_GPU_LANE_MID=1
+ * routes values up to 64 KiB through the mid-class kernels as well. */
+bool lzf_lane_compress_supported(uint32_t max_len)
+{
+    if (max_len <= KS_MAXN) return true;
+    const char *e = getenv("LZF_GPU_LANE_MID");
+    return max_len <= KM_MAXN && e && *e == '1';
+}
 
 hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scratch,
                                     size_t scratch_bytes, uint32_t force_fix, hipStream_t aux,

@@ -144,7 +144,7 @@ def test_unaligned_arenas(oracle, generation, align):
     rnd = random.Random(align)
     vals, caps = [], []
     for i in range(600):
-        n = rnd.choice([1, 2, 3, 4, 5, 17, 33, 64, 700, 4096, 5003])
+        n = rnd.choice([1, 2, 3, 4, 5, 17, 33, 64, 700, 4095, 4096])   # one size class
         vals.append(synth(rnd.randrange(6), 0x5EED00C0, i, n))
         caps.append(rnd.choice([max(1, n - 4), n + n // 16 + 64, rnd.randint(1, n + 8)]))
     res = gpu_compress(vals, caps, align=align)
@@ -156,6 +156,17 @@ def test_unaligned_arenas(oracle, generation, align):
     assert gpu_decompress(streams, [len(v) for v in origs], align=align) == [(v, 0) for v in origs]
 
 
+def test_lane_mid_class(oracle, monkeypatch):
+    # the mid-class lane kernels (values 4 KiB .. 64 KiB), opt-in
+    from tests.gpu_batch import gpu_compress
+    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.setenv("LZF_GPU_LANE_MID", "1")
+    rnd = random.Random(21)
+    vals = [synth(rnd.randrange(6), 0x5EED00F0, i, rnd.randint(1, 20000)) for i in range(300)]
+    caps = [rnd.choice([max(1, len(v) - 4), len(v) + len(v) // 16 + 64]) for v in vals]
+    assert gpu_compress(vals, caps, align=3) == [oracle.compress(v, c) for v, c in zip(vals, caps)]
+
+
 def test_lane_order_repair_path(oracle, monkeypatch):
     # the repair path of the bucket-head atomics (taken when the LDS does not
     # serialise a wave's same-address atomics in lane order) gives the same
@@ -163,6 +174,7 @@ def test_lane_order_repair_path(oracle, monkeypatch):
     from tests.gpu_batch import gpu_compress
     monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
     monkeypatch.setenv("LZF_GPU_LANE_FORCE_FIX", "1")
+    monkeypatch.setenv("LZF_GPU_LANE_MID", "1")
     rnd = random.Random(3)
     for nmax in (4096, 20000):
         vals = [synth(rnd.randrange(6), 0x5EED00D0, i, rnd.randint(1, nmax)) for i in range(200)]
@@ -170,7 +182,7 @@ def test_lane_order_repair_path(oracle, monkeypatch):
         assert gpu_compress(vals, caps) == [oracle.compress(v, c) for v, c in zip(vals, caps)]
 
 
-@pytest.mark.parametrize("nmax", [8192, 9000])
+@pytest.mark.parametrize("nmax", [4096, 8192, 9000])
 def test_random_differential(oracle, generation, nmax):
     # nmax 8192: the batch fits the non-wrapping ring/chain kernel; 9000:
     # the wrapping one (the kernel is chosen per batch from max_len)
