@@ -608,9 +608,8 @@ __global__ __launch_bounds__(64) void lzf_cand_mid_kernel(LzfBatch bt, LzfLaneSc
 
 /* Diagnostic build only (-DK2_COUNT_SITES): per-site event counts of the
  * parse kernel's global memory accesses, summed over all lanes. */
-#ifdef K2_COUNT_SITES
+#if defined(K2_COUNT_SITES) || defined(KW_PHASES)
 __device__ unsigned long long k2_sites[16];
-#define K2_SITE(i) atomicAdd(&k2_sites[i], 1ull)
 extern "C" int lzf_gpu_debug_sites(unsigned long long *out16, int reset)
 {
     hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(k2_sites), sizeof(k2_sites));
@@ -620,8 +619,17 @@ extern "C" int lzf_gpu_debug_sites(unsigned long long *out16, int reset)
     }
     return e == hipSuccess ? 0 : -2;
 }
+#endif
+#ifdef K2_COUNT_SITES
+#define K2_SITE(i) atomicAdd(&k2_sites[i], 1ull)
 #else
 #define K2_SITE(i) ((void)0)
+#endif
+/* -DKW_PHASES: cycles per phase of the wave-form parse, summed in k2_sites[0..7] */
+#ifdef KW_PHASES
+#define KW_PH(i) do { const uint64_t t_ = clock64(); ph_[i] += t_ - ph_t; ph_t = t_; } while (0)
+#else
+#define KW_PH(i) ((void)0)
 #endif
 
 /* m = min(first mismatch >= start, lim), bytes [0, start) known equal
@@ -884,6 +892,309 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
 #undef K2_RING
 }
 
+/* ======================================================================== */
+/* compress, kernel 2 (wave form): the parse 64 positions at a time         */
+/* ======================================================================== */
+
+/* One wave per value of the small class; the value's bytes, its cand words
+ * and an inserted-bitmap live in LDS.  Per window of 64 positions from the
+ * parse position P every lane decides its position as if the parse visited
+ * it: its ref is the first inserted position on the cand chain, literal or
+ * match, and the match length (cand agreement, else an 8-byte probe).  A
+ * candidate before P is checked in the bitmap (decided); one inside the
+ * window is assumed inserted.  The scalar unit then follows the parse's
+ * orbit P -> P + step -> ... jumping over runs of literal lanes; lanes it
+ * stops at that still need work get it there, so only visited positions pay
+ * for it: a candidate found skipped is walked back along its cand chain, a
+ * match longer than the probe is measured by the whole wave (256 bytes at
+ * once).  A visited lane whose in-window candidate turns out to lie in a
+ * match interior (not inserted: src/lzf_c.c:227-247) ends the window there,
+ * so every emitted token is the reference's.  Emission is closed form over
+ * the window's tokens (prefix sum of output sizes; a run's header is written
+ * when the run closes) with the reference's out-of-space checks. */
+#define KW_MAXN KS_MAXN
+
+/* lane states of a window */
+#define KW_LIT   0u    /* literal */
+#define KW_MATCH 1u    /* match of length m */
+#define KW_LONG  2u    /* match of length >= k (k < lim), to be measured */
+#define KW_WALK  3u    /* candidate q not inserted: walk the chain first */
+
+/* literal or match at x given the ref q and its rel code (src/lzf_c.c:151-209) */
+__device__ __forceinline__ void kw_decide(const uint32_t *Bw, uint32_t n, uint32_t x, bool act, uint32_t rel,
+                                          uint32_t q, uint32_t &st, uint32_t &m, uint32_t &k, uint32_t &lim)
+{
+    st = KW_LIT;
+    m = 1u;
+    if (!(act && rel >= 2u && x + 4u < n)) return;
+    uint32_t maxlen = n - x - 2u;                                     /* src/lzf_c.c:169-170 */
+    if (maxlen > LZF_MAX_REF) maxlen = LZF_MAX_REF;
+    lim = (maxlen > 16u && maxlen < 19u) ? 19u : maxlen;
+    st = KW_MATCH;
+    if (rel <= 6u) {
+        m = rel + 1u < lim ? rel + 1u : lim;
+        return;
+    }
+    k = rel == 7u ? 8u : 3u;
+    const uint32_t d0 = ks_rd4(Bw, x + k) ^ ks_rd4(Bw, q + k);
+    const uint32_t d1 = ks_rd4(Bw, x + k + 4u) ^ ks_rd4(Bw, q + k + 4u);
+    if (d0) k += (uint32_t)__builtin_ctz(d0) >> 3;
+    else if (d1) k += 4u + ((uint32_t)__builtin_ctz(d1) >> 3);
+    else k += 8u;
+    if (!(d0 | d1) && k < lim) st = KW_LONG;
+    m = k < lim ? k : lim;
+}
+
+/* one link back along the cand chain from a skipped q */
+__device__ __forceinline__ bool kw_hop(const uint16_t *Cw, uint32_t x, uint32_t &rel, uint32_t &q)
+{
+    K2_SITE(12);
+    const uint32_t c2 = Cw[q], r2 = c2 >> 13, q2 = q - 1u - (c2 & 0x1FFFu);
+    if (!r2 || x - q2 - 1u >= LZF_WINDOW) {
+        rel = 0u;
+        return false;
+    }
+    const bool e1 = rel >= 2u && rel <= 8u, e2 = r2 >= 2u;
+    rel = rel == 9u ? 9u : (e1 && e2) ? 8u : (e1 != e2) ? 1u : 9u;
+    q = q2;
+    return true;
+}
+
+/* first inserted position on the cand chain from q (q < P: the bitmap is
+ * final there); rel follows it: 8 equal (length unknown), 1 differ, 0 none.
+ * A skipped position below P is never visited, so its cand word serves only
+ * walks through it: the walk's start q0 is pointed straight at the result
+ * (path compression; code 2 = 3 bytes equal, 1 = differ, 0 = none). */
+__device__ __forceinline__ void kw_walk(const uint32_t *Bw, uint16_t *Cw, const uint32_t *IB, uint32_t x,
+                                        uint32_t &rel, uint32_t &q, uint32_t q0)
+{
+    while (!((IB[q >> 5] >> (q & 31u)) & 1u)) {
+        if (!kw_hop(Cw, x, rel, q)) {
+            Cw[q0] = 0u;
+            return;
+        }
+    }
+    if (q != q0) {
+        const bool eq = ((ks_rd4(Bw, q0) ^ ks_rd4(Bw, q)) & 0xFFFFFFu) == 0u;
+        Cw[q0] = (uint16_t)(((eq ? 2u : 1u) << 13) | (q0 - q - 1u));
+    }
+    if (rel == 9u) rel = ((ks_rd4(Bw, x) ^ ks_rd4(Bw, q)) & 0xFFFFFFu) == 0u ? 8u : 1u;
+}
+__device__ __forceinline__ unsigned long long kw_range(uint32_t a, uint32_t b)   /* bits [a, b), a < 64 */
+{
+    const unsigned long long hi = b >= 64u ? ~0ull : (1ull << b) - 1ull;
+    return hi & ~((1ull << a) - 1ull);
+}
+
+__global__ __launch_bounds__(64) void lzf_parse_wave_kernel(LzfBatch bt, LzfLaneScratch sc)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t Bw[KW_MAXN / 4u + 8u];
+    __shared__ __attribute__((aligned(16))) uint16_t Cw[KW_MAXN + 64u];
+    __shared__ uint32_t IB[KW_MAXN / 32u + 4u];
+    const uint32_t lane = threadIdx.x, v = blockIdx.x;
+    const unsigned long long mine = 1ull << lane, lt = mine - 1ull;
+    const uint32_t n = bt.in_len[v], cap = bt.out_cap[v];
+    if (n == 0u || cap == 0u) {                                       /* src/lzf_c.c:131 */
+        if (lane == 0u) bt.out_len[v] = 0u;
+        return;
+    }
+    const uint8_t *src = bt.in + bt.in_off[v];
+    uint8_t *dst = bt.out + bt.out_off[v];
+    const uint32_t np = n >= 3u ? n - 2u : 0u;                        /* positions 0 .. n-3 */
+#ifdef KW_PHASES
+    uint64_t ph_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ph_t = clock64();
+#endif
+    {
+        const uint4 *cand = (const uint4 *)(sc.cand + (uint64_t)v * sc.cstride);
+        for (uint32_t k = lane; k < (KW_MAXN / 4u + 8u) / 4u; k += 64u) {
+            const uint32_t at = 16u * k;
+            ((uint4 *)Bw)[k] = at < n ? ln_ld16_safe(src + at, n - at) : make_uint4(0, 0, 0, 0);
+        }
+        for (uint32_t k = lane; k < (np + 7u) / 8u; k += 64u) ((uint4 *)Cw)[k] = cand[k];
+        for (uint32_t k = lane; k < KW_MAXN / 32u + 4u; k += 64u) IB[k] = 0u;
+    }
+    __syncthreads();
+    KW_PH(0);
+#define KW_BYTE(x_) ((Bw[(x_) >> 2] >> (8u * ((x_) & 3u))) & 0xFFu)
+    uint32_t P = 0u, o = 1u, run = 0u;                                /* op, lit of the reference */
+    bool ok = true;
+    while (P < np) {
+        if (lane == 0u) K2_SITE(11);
+        const uint32_t x = P + lane;
+        const bool act = x < np;
+        const uint32_t c = act ? (uint32_t)Cw[x] : 0u;
+        /* rel: 0 no ref; 1 ref with other bytes; 2..6 equal for rel+1 bytes;
+         * 7 equal >= 8; 8 equal 3 bytes, length unknown; 9 unknown */
+        uint32_t rel = c >> 13;
+        uint32_t q = x - 1u - (c & 0x1FFFu);
+        const bool spec = rel != 0u && q >= P;                        /* assumed inserted */
+        uint32_t st = KW_LIT, m = 1u, k = 0u, lim = 0u;
+        const uint32_t q1 = q;
+        bool walk = rel != 0u && !spec && !((IB[q >> 5] >> (q & 31u)) & 1u);
+        if (walk) {                                                   /* one link back, all lanes */
+            walk = kw_hop(Cw, x, rel, q) && !((IB[q >> 5] >> (q & 31u)) & 1u);
+            if (!walk && rel == 9u) rel = ((ks_rd4(Bw, x) ^ ks_rd4(Bw, q)) & 0xFFFFFFu) == 0u ? 8u : 1u;
+        }
+        if (walk) st = KW_WALK;
+        else kw_decide(Bw, n, x, act, rel, q, st, m, k, lim);
+        KW_PH(1);
+        /* the orbit of the parse through the window: runs of literal lanes
+         * are taken at once, the scalar loop stops at the other lanes */
+        const uint32_t end = np - P < 64u ? np - P : 64u;             /* lanes that are positions */
+        unsigned long long STOP = __ballot(st != KW_LIT), V = 0ull;
+        uint32_t t = 0u;
+        while (true) {
+            const unsigned long long rest = STOP & ~((1ull << t) - 1ull);
+            const uint32_t u = rest ? (uint32_t)__builtin_ctzll(rest) : 64u;
+            if (u >= end) {
+                V |= kw_range(t, end);
+                t = end;
+                break;
+            }
+            V |= kw_range(t, u + 1u);
+            if (lane == 0u) K2_SITE(15);
+            uint32_t su = (uint32_t)__builtin_amdgcn_readlane((int)st, (int)u);
+            if (su == KW_WALK) {                                      /* skipped candidate */
+                KW_PH(2);
+                if (lane == 0u) K2_SITE(10);
+                if (lane == u) {
+                    kw_walk(Bw, Cw, IB, x, rel, q, q1);
+                    kw_decide(Bw, n, x, act, rel, q, st, m, k, lim);
+                }
+                su = (uint32_t)__builtin_amdgcn_readlane((int)st, (int)u);
+                KW_PH(6);
+            }
+            if (su == KW_LONG) {                                      /* the wave measures it */
+                KW_PH(2);
+                if (lane == 0u) K2_SITE(13);
+                const uint32_t xu = P + u;
+                const uint32_t qu = (uint32_t)__builtin_amdgcn_readlane((int)q, (int)u);
+                const uint32_t ku = (uint32_t)__builtin_amdgcn_readlane((int)k, (int)u);
+                const uint32_t lu = (uint32_t)__builtin_amdgcn_readlane((int)lim, (int)u);
+                const uint32_t at = ku + 4u * lane;
+                const uint32_t dd = at < lu ? ks_rd4(Bw, xu + at) ^ ks_rd4(Bw, qu + at) : 0xFFu;
+                const unsigned long long dm = __ballot(dd != 0u);
+                uint32_t mu = lu;
+                if (dm) {
+                    const uint32_t j = (uint32_t)__builtin_ctzll(dm);
+                    const uint32_t dj = (uint32_t)__builtin_amdgcn_readlane((int)dd, (int)j);
+                    const uint32_t e = ku + 4u * j + ((uint32_t)__builtin_ctz(dj) >> 3);
+                    mu = e < lu ? e : lu;
+                }
+                if (lane == u) {
+                    m = mu;
+                    st = KW_MATCH;
+                }
+                su = KW_MATCH;
+                KW_PH(7);
+            }
+            t = su == KW_LIT ? u + 1u : u + (uint32_t)__builtin_amdgcn_readlane((int)m, (int)u);
+            if (t >= end) break;
+        }
+        KW_PH(2);
+        const bool hit = st != KW_LIT;                                /* every visited lane is final */
+        const unsigned long long HITm = __ballot(hit);
+        const bool isv = (V >> lane) & 1ull;
+        const uint32_t s = ks_hibit(V & (lt | mine));                 /* latest token <= lane */
+        const uint32_t m_s = (uint32_t)__shfl((int)m, (int)s);
+        const bool inm = !isv && ((HITm >> s) & 1ull);                /* inside s's match */
+        const unsigned long long IM = __ballot(inm && lane + 2u < s + m_s);
+        const unsigned long long INV = V & __ballot(spec && ((IM >> (q - P)) & 1ull));
+        const uint32_t f = INV ? (uint32_t)__builtin_ctzll(INV) : 64u;
+        if (lane == 0u && f < 64u) K2_SITE(14);
+        const unsigned long long keep = f < 64u ? (1ull << f) - 1ull : ~0ull;
+        const unsigned long long TK = V & keep;
+        const unsigned long long INS = __ballot(isv || (inm && lane + 2u >= s + m_s)) & keep;
+        KW_PH(3);
+
+        /* emission (src/lzf_c.c:172-224, 258-273) */
+        const bool tok = (TK >> lane) & 1ull;
+        const unsigned long long Mb = TK & HITm, Lb = TK & ~HITm, mlt = Mb & lt;
+        const unsigned long long seg = mlt ? lt & ~((2ull << ks_hibit(mlt)) - 1ull) : lt;
+        const uint32_t lb = (uint32_t)__builtin_popcountll(Lb & seg);
+        const uint32_t r0 = (mlt ? 0u : run) + lb;                    /* open run before lane */
+        const uint32_t rl = r0 & 31u;
+        /* output bytes of a token: literal 1 (+1 on a rollover); match 3
+         * (+1 long form, -1 when it undoes an empty run): prefix sums as
+         * lane-mask popcounts */
+        const unsigned long long RL = __ballot(tok && !hit && ((r0 + 1u) & 31u) == 0u);
+        const unsigned long long BG = __ballot(tok && hit && m - 2u >= 7u);
+        const unsigned long long UD = __ballot(tok && hit && rl == 0u);
+#define KW_MB(M_) __builtin_amdgcn_mbcnt_hi((uint32_t)((M_) >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)(M_), 0u))
+        const uint32_t ob = o + KW_MB(TK) + KW_MB(RL) + 2u * KW_MB(Mb) + KW_MB(BG) - KW_MB(UD);
+#undef KW_MB
+        const uint32_t osum = (uint32_t)(__builtin_popcountll(TK) + __builtin_popcountll(RL) +
+                                         2 * __builtin_popcountll(Mb) + __builtin_popcountll(BG) -
+                                         __builtin_popcountll(UD));
+        const uint32_t om = ob - (rl == 0u ? 1u : 0u);
+        const bool bad = tok && (hit ? om + 4u >= cap : ob >= cap);   /* src/lzf_c.c:176, 263 */
+        KW_PH(4);
+        if (__ballot(bad)) {
+            ok = false;
+            break;
+        }
+        if (tok) {
+            if (!hit) {
+                dst[ob] = (uint8_t)KW_BYTE(x);
+                if (((r0 + 1u) & 31u) == 0u) dst[ob - LZF_MAX_LIT] = (uint8_t)(LZF_MAX_LIT - 1u);
+            } else {
+                const uint32_t off = x - q - 1u, L = m - 2u;
+                if (rl) dst[ob - rl - 1u] = (uint8_t)(rl - 1u);       /* close the run */
+                if (L < 7u) {
+                    dst[om] = (uint8_t)((off >> 8) | (L << 5));
+                    dst[om + 1u] = (uint8_t)off;
+                } else {
+                    dst[om] = (uint8_t)(0xE0u | (off >> 8));
+                    dst[om + 1u] = (uint8_t)(L - 7u);
+                    dst[om + 2u] = (uint8_t)off;
+                }
+            }
+        }
+        /* inserted positions of the window; a match past the window inserts
+         * its two last positions (src/lzf_c.c:227-247) */
+        if (lane < 3u) {
+            const uint32_t sh = P & 31u;
+            const unsigned long long lo = INS << sh;
+            const uint32_t w = lane == 0u ? (uint32_t)lo : lane == 1u ? (uint32_t)(lo >> 32)
+                                                                      : (sh ? (uint32_t)(INS >> (64u - sh)) : 0u);
+            if (w) IB[(P >> 5) + lane] |= w;
+        }
+        const uint32_t last = ks_hibit(TK);
+        if (f == 64u && lane == last && hit && lane + m > 64u) {
+            const uint32_t t1 = x + m - 2u, t2 = t1 + 1u;
+            if (lane + m - 2u >= 64u) IB[t1 >> 5] |= 1u << (t1 & 31u);
+            IB[t2 >> 5] |= 1u << (t2 & 31u);
+        }
+        o += osum;
+        run = ((HITm >> last) & 1ull) ? 0u : (((uint32_t)__builtin_amdgcn_readlane((int)r0, (int)last) + 1u) & 31u);
+        P = f < 64u ? P + f : P + t;
+        KW_PH(5);
+        ln_wave_fence();
+    }
+#ifdef KW_PHASES
+    if (lane == 0u)
+        for (uint32_t i = 0; i < 8u; i++) atomicAdd(&k2_sites[i], (unsigned long long)ph_[i]);
+#endif
+    if (lane == 0u) {
+        if (!ok || o + 3u > cap) {                                    /* src/lzf_c.c:276 */
+            bt.out_len[v] = 0u;
+        } else {
+            for (uint32_t p = P; p < n; p++) {                        /* src/lzf_c.c:279-288 */
+                dst[o++] = (uint8_t)KW_BYTE(p);
+                if (++run == LZF_MAX_LIT) {
+                    dst[o - LZF_MAX_LIT - 1u] = (uint8_t)(LZF_MAX_LIT - 1u);
+                    run = 0u;
+                    o++;
+                }
+            }
+            if (run) dst[o - run - 1u] = (uint8_t)(run - 1u);
+            else o--;
+            bt.out_len[v] = o;
+        }
+    }
+#undef KW_BYTE
+}
+
 /* ---- launcher ------------------------------------------------------------ */
 
 static uint64_t lane_cstride(uint32_t max_len) { return (((uint64_t)max_len + 7u) & ~7ull) + 8u; }
@@ -943,11 +1254,17 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
             hipFuncGetAttributes(&fa, (const void *)lzf_cand_small_kernel) == hipSuccess && cus > 0 &&
             fa.sharedSizeBytes > 0) {
             uint32_t per = (uint32_t)(160u * 1024u / fa.sharedSizeBytes);   /* LDS-bound residency */
+            const char *pe_ = getenv("LZF_LANE_CAND_PER");            /* residency override */
+            if (pe_ && atoi(pe_) > 0) per = (uint32_t)atoi(pe_);
             if (per > 32u) per = 32u;
             if (per < 1u) per = 1u;
             small_grid = (uint32_t)cus * per;
         }
     }
+    /* kernel 2: one lane per value; LZF_GPU_LANE_PARSE=wave selects the wave
+     * form for the small class (slower today) */
+    const char *pe = getenv("LZF_GPU_LANE_PARSE");
+    const bool wave_parse = b.max_len <= KW_MAXN && pe && pe[0] == 'w';
     const size_t parse_lds = lane_lds_for("LZF_LANE_PARSE_BLOCKS", 0u);
     if (parse_lds) {
         hipError_t e = hipFuncSetAttribute((const void *)lzf_parse_lane_kernel,
@@ -981,8 +1298,11 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
             if ((e = hipStreamWaitEvent(aux, ev[h], 0)) != hipSuccess) return e;
             s2 = aux;
         }
-        hipLaunchKernelGGL(lzf_parse_lane_kernel, dim3((cnt + K2_THREADS - 1u) / K2_THREADS),
-                           dim3(K2_THREADS), parse_lds, s2, c, sc[h]);
+        if (wave_parse)
+            hipLaunchKernelGGL(lzf_parse_wave_kernel, dim3(cnt), dim3(64), 0, s2, c, sc[h]);
+        else
+            hipLaunchKernelGGL(lzf_parse_lane_kernel, dim3((cnt + K2_THREADS - 1u) / K2_THREADS),
+                               dim3(K2_THREADS), parse_lds, s2, c, sc[h]);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (pipe && (e = hipEventRecord(ev[2 + h], aux)) != hipSuccess) return e;
     }

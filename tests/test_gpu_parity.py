@@ -167,6 +167,20 @@ def test_lane_mid_class(oracle, monkeypatch):
     assert gpu_compress(vals, caps, align=3) == [oracle.compress(v, c) for v, c in zip(vals, caps)]
 
 
+@pytest.mark.parametrize("align", [16, 3])
+def test_wave_parse(oracle, monkeypatch, align):
+    # the wave form of the parse kernel (64 positions per step, opt-in):
+    # every size class edge of a window, caps that run out inside a window
+    from tests.gpu_batch import gpu_compress
+    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.setenv("LZF_GPU_LANE_PARSE", "wave")
+    rnd = random.Random(77 + align)
+    vals = [synth(rnd.randrange(6), 0x5EED00E0, i, rnd.randint(1, 4096)) for i in range(400)]
+    vals += [synth(k, 0x5EED00E1, n, n) for k in range(6) for n in (1, 2, 3, 4, 5, 63, 64, 65, 66, 67, 130)]
+    caps = [rnd.choice([max(1, len(v) - 4), len(v) + len(v) // 16 + 64, rnd.randint(1, len(v) + 8)]) for v in vals]
+    assert gpu_compress(vals, caps, align=align) == [oracle.compress(v, c) for v, c in zip(vals, caps)]
+
+
 def test_lane_order_repair_path(oracle, monkeypatch):
     # the repair path of the bucket-head atomics (taken when the LDS does not
     # serialise a wave's same-address atomics in lane order) gives the same

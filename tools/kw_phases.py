@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
-"""Per-site access counts of the lane parse kernel (diagnostic build
-gibson_amd/liblzf_hip_sites.so, -DK2_COUNT_SITES), per value."""
+"""Cycles per phase of the wave-form parse kernel (diagnostic build with
+-DKW_PHASES, tools/build_variant.sh), per value."""
 import ctypes
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["LZF_HIP_LIB"] = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gibson_amd",
-                                         "liblzf_hip_sites.so")
+lib = sys.argv[5] if len(sys.argv) > 5 else "liblzf_hip_phases.so"
+os.environ["LZF_HIP_LIB"] = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gibson_amd", lib)
 os.environ["LZF_GPU_LANE_PIPE"] = "0"
 import torch  # noqa: E402
 
@@ -30,9 +30,8 @@ L.lzf_gpu_debug_sites(buf, 1)
 gibson_amd.compress_batch(src, off, ln, out, off, cap, olen, n)
 torch.cuda.synchronize()
 L.lzf_gpu_debug_sites(buf, 0)
-names = ["lane-iterations", "C load", "C2 use", "bits load", "walk cand load", "eq3", "input window",
-         "extend piece", "out dword", "wave: walk stops", "steps", "wave: windows", "wave: walk hops",
-         "wave: long measures", "wave: truncations", "wave: orbit stops"]
+names = ["stage", "decide", "orbit", "validate", "emit scan", "store+update", "orbit: walks", "orbit: long"]
+tot = sum(buf[i] for i in range(8))
 for i, nm in enumerate(names):
-    if nm != "-":
-        print(f"{nm:16s} {buf[i] / count:10.1f} per value")
+    print(f"{nm:18s} {buf[i] / count:12.0f} cycles/value  {100.0 * buf[i] / max(tot, 1):5.1f}%")
+print(f"{'total':18s} {tot / count:12.0f}")

@@ -40,7 +40,7 @@ int main(int argc, char **argv)
     uint8_t *ins = malloc(n);
     uint64_t steps = 0, lits = 0, matches = 0, walks = 0, hops = 0, maxhop = 0, mism = 0;
     uint64_t dist_hist[6] = {0}, mlen_hist[8] = {0}, backd[6] = {0};
-    uint64_t k1hops = 0, k1max_win = 0, k1first = 0, maxsteps = 0;
+    uint64_t wins = 0, truncs = 0, k1hops = 0, k1max_win = 0, k1first = 0, maxsteps = 0;
     for (uint32_t v = 0; v < count; v++) {
         syn_generate(kind, 0x5EED0002ull + kind, v, b, n);
         memset(tab, 0xFF, 65536 * 4);
@@ -104,6 +104,35 @@ int main(int argc, char **argv)
             tab[slot(b, p - 1)] = p - 1; ins[p - 1] = 1;
         }
         (void)me;
+        /* window-parse model: replay the parse in 64-position windows; a window
+         * ends at its first token >= P+64 or early at the first token whose
+         * same-slot predecessor lies inside the window but in a match interior */
+        {
+            uint8_t *ins2 = calloc(n, 1);
+            uint32_t *tab2 = malloc(65536 * 4);
+            memset(tab2, 0xFF, 65536 * 4);
+            uint32_t pp = 0, P = 0;
+            wins++;
+            while (n >= 3 && pp < n - 2) {
+                if (pp >= P + 64) { P = pp; wins++; }
+                uint32_t q1 = cand[pp];
+                if (q1 != NONE && q1 >= P && pp > P && !ins2[q1]) { P = pp; wins++; truncs++; }
+                uint32_t s = slot(b, pp), r = tab2[s];
+                tab2[s] = pp; ins2[pp] = 1;
+                int hit = r != NONE && (pp - r - 1u) < 8192 && pp + 4 < n && r > 0 &&
+                          b[r] == b[pp] && b[r + 1] == b[pp + 1] && b[r + 2] == b[pp + 2];
+                if (!hit) { pp++; continue; }
+                uint32_t maxlen = n - pp - 2;
+                if (maxlen > 264) maxlen = 264;
+                uint32_t lim = maxlen > 16 && maxlen < 19 ? 19 : maxlen, m = 3;
+                while (m < lim && b[r + m] == b[pp + m]) m++;
+                pp += m;
+                if (pp >= n - 2) break;
+                tab2[slot(b, pp - 2)] = pp - 2; ins2[pp - 2] = 1;
+                tab2[slot(b, pp - 1)] = pp - 1; ins2[pp - 1] = 1;
+            }
+            free(ins2); free(tab2);
+        }
         steps += vs;
         if (vs > maxsteps) maxsteps = vs;
     }
@@ -121,5 +150,6 @@ int main(int argc, char **argv)
     for (int i = 0; i < 5; i++) printf(" %.1f", backd[i] / c);
     printf("\nkernel-1 bucket hops/position %.3f, max-over-window %.2f per 64-window\n",
            (double)k1hops / (steps ? (double)n * count : 1.0), (double)k1max_win / k1first);
+    printf("window parse: windows/value %.1f  truncated %.1f\n", wins / c, truncs / c);
     return 0;
 }
