@@ -116,19 +116,20 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
         const uint32_t tsz = c < 32u ? c + 2u : ((c >> 5) == 7u ? 3u : 2u);
         uint32_t nx = lane + tsz;
         if (ip + tsz >= in_len || nx > CD_LANES) nx = CD_LANES;   /* loop ends / next round */
-        uint32_t J0 = nx, J1, J2, J3, J4, J5;
+        /* every token takes >= 2 input bytes, so a round has <= 32 tokens:
+         * lane l < 32 finds the start of token l with 5 doubling levels */
+        uint32_t J0 = nx, J1, J2, J3, J4;
         J1 = J0 >= CD_LANES ? CD_LANES : (uint32_t)__shfl((int)J0, (int)J0);
         J2 = J1 >= CD_LANES ? CD_LANES : (uint32_t)__shfl((int)J1, (int)J1);
         J3 = J2 >= CD_LANES ? CD_LANES : (uint32_t)__shfl((int)J2, (int)J2);
         J4 = J3 >= CD_LANES ? CD_LANES : (uint32_t)__shfl((int)J3, (int)J3);
-        J5 = J4 >= CD_LANES ? CD_LANES : (uint32_t)__shfl((int)J4, (int)J4);
         uint32_t x = 0, y;
         y = (uint32_t)__shfl((int)J0, (int)(x & 63u)); if ((lane & 1u) && x < CD_LANES) x = y;
         y = (uint32_t)__shfl((int)J1, (int)(x & 63u)); if ((lane & 2u) && x < CD_LANES) x = y;
         y = (uint32_t)__shfl((int)J2, (int)(x & 63u)); if ((lane & 4u) && x < CD_LANES) x = y;
         y = (uint32_t)__shfl((int)J3, (int)(x & 63u)); if ((lane & 8u) && x < CD_LANES) x = y;
         y = (uint32_t)__shfl((int)J4, (int)(x & 63u)); if ((lane & 16u) && x < CD_LANES) x = y;
-        y = (uint32_t)__shfl((int)J5, (int)(x & 63u)); if ((lane & 32u) && x < CD_LANES) x = y;
+        if (lane >= 32u) x = CD_LANES;
         flag[lane] = 0u;
         cd_fence();
         if (x < CD_LANES) flag[x] = 1u;
@@ -150,10 +151,12 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
             olen = len + 2u;
             back = ((c & 31u) << 8) + offb + 1u;
         }
-        const uint32_t tinfo = lit ? lsrc : back;          /* literal source / distance */
+        /* the owner's info for an output byte o: literal -> input ring index
+         * o + (lsrc - Ot), flagged in bit 31; back-ref -> distance */
         const uint32_t ol = tok ? olen : 0u;
         const uint32_t incl = cd_incl_sum(ol);
         const uint32_t Ot = O + incl - ol;                 /* output offset of my token */
+        const uint32_t tinfo = lit ? (((lsrc - Ot) & 0x7FFFFFFFu) | 0x80000000u) : back;
         /* ---- 3. the reference's checks, in its order ------------------ */
         if (tok) {
             if (lit) {
@@ -190,16 +193,14 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
             carry = cd_rl(k, 63u);
             const uint32_t o = gb + lane;
             const bool live = g + lane < total;
-            const uint32_t tO = (uint32_t)__shfl((int)Ot, (int)k);
-            const uint32_t tLit = (uint32_t)__shfl((int)lit, (int)k);
-            const uint32_t tSrc = (uint32_t)__shfl((int)tinfo, (int)k);
+            const uint32_t tInf = (uint32_t)__shfl((int)tinfo, (int)k);
             uint32_t val = 0;
             int ptr = -1;
             if (live) {
-                if (tLit) {
-                    val = inr[(tSrc + (o - tO)) & imask];
+                if (tInf >> 31) {
+                    val = inr[(o + tInf) & imask];
                 } else {
-                    const uint32_t so = o - tSrc;
+                    const uint32_t so = o - tInf;
                     if (so >= gb) ptr = (int)(so - gb);
                     else val = outr[so & omask];
                 }

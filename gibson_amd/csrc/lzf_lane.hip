@@ -660,6 +660,10 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
     uint64_t acc = 0;
     uint32_t accn = dm, fw = 0;
     uint32_t hx = dm;                   /* header byte of the open run (index from da) */
+    /* completed dwords [fs, fw) wait in pb0..2 and go out as one 16-byte
+     * store: every store instruction of the wave touches 64 lines (one
+     * per lane's value), so fewer, wider stores */
+    uint32_t pb0 = 0u, pb1 = 0u, pb2 = 0u, fs = 0u;
     /* input: 16-byte window of aligned block wb (+ the next block) */
     const uint32_t sm = (uint32_t)((uintptr_t)src & 15u);
     const uint8_t *const sa = src - sm;
@@ -687,13 +691,24 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
         accn += (cnt_);                                                            \
         if (accn >= 4u) {                                                          \
             const uint32_t w_ = (uint32_t)acc;                                     \
-            uint8_t *a_ = da + 4u * fw;                                            \
-            if (fw != 0u || dm == 0u) {                                            \
-                *(uint32_t *)a_ = w_;                                              \
+            if (fw == 0u && dm != 0u) {        /* the partial first dword */       \
+                for (uint32_t t_ = dm; t_ < 4u; t_++) da[t_] = (uint8_t)(w_ >> (8u * t_)); \
+                fs = 1u;                                                           \
             } else {                                                               \
-                for (uint32_t t_ = dm; t_ < 4u; t_++) a_[t_] = (uint8_t)(w_ >> (8u * t_)); \
+                const uint32_t np_ = fw - fs;                                      \
+                if (np_ == 3u) {                                                   \
+                    const uint4 v_ = make_uint4(pb0, pb1, pb2, w_);                \
+                    __builtin_memcpy(da + 4u * fs, &v_, 16);                       \
+                    K2_SITE(8);                                                    \
+                    fs = fw + 1u;                                                  \
+                } else if (np_ == 0u) {                                            \
+                    pb0 = w_;                                                      \
+                } else if (np_ == 1u) {                                            \
+                    pb1 = w_;                                                      \
+                } else {                                                           \
+                    pb2 = w_;                                                      \
+                }                                                                  \
             }                                                                      \
-            K2_SITE(8);                                                            \
             fw++;                                                                  \
             acc >>= 32;                                                            \
             accn -= 4u;                                                            \
@@ -704,6 +719,12 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
         if ((x_) >= 4u * fw) {                                                     \
             const uint32_t sh_ = 8u * ((x_) - 4u * fw);                            \
             acc = (acc & ~(0xFFull << sh_)) | ((uint64_t)(byte_) << sh_);          \
+        } else if ((x_) >= 4u * fs) {                                              \
+            const uint32_t i_ = ((x_) >> 2) - fs, sh_ = 8u * ((x_) & 3u);          \
+            const uint32_t mk_ = ~(0xFFu << sh_), b_ = (uint32_t)(byte_) << sh_;  \
+            if (i_ == 0u) pb0 = (pb0 & mk_) | b_;                                  \
+            else if (i_ == 1u) pb1 = (pb1 & mk_) | b_;                             \
+            else pb2 = (pb2 & mk_) | b_;                                           \
         } else {                                                                   \
             da[(x_)] = (uint8_t)(byte_);                                           \
         }                                                                          \
@@ -882,6 +903,8 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
     }
     if (run) K2_PATCH(hx, run - 1u);
     else o--;
+    for (uint32_t i = fs; i < fw; i++)
+        *(uint32_t *)(da + 4u * i) = i == fs ? pb0 : i == fs + 1u ? pb1 : pb2;
     for (uint32_t t = 0; t < accn; t++)
         if (4u * fw + t >= dm) da[4u * fw + t] = (uint8_t)(acc >> (8u * t));
     bt.out_len[v] = o;

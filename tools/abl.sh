@@ -7,5 +7,5 @@ for lib in "$@"; do
     LZF_HIP_LIB=$PWD/gibson_amd/$lib LZF_GPU_LANE_PIPE=0 timeout -k 10 200 rocprofv3 --kernel-trace --stats \
         --output-format csv -d gpurun_out/abl/$lib -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu \
         > gpurun_out/abl/$lib.log 2>&1 || exit 1
-    python3 profiles/summarize.py gpurun_out/abl/$lib x | grep -E "lzf_(cand|parse)"
+    python3 profiles/summarize.py gpurun_out/abl/$lib x | grep -E "lzf_(cand|parse|decomp)"
 done
