@@ -402,7 +402,6 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
     while (v < bt.count) {
         const uint32_t n = pn;
         uint16_t *cand = sc.cand + (uint64_t)v * sc.cstride;
-        uint32_t *bits = sc.bits + (uint64_t)v * sc.bstride;
 #pragma unroll
         for (uint32_t k = 0; k < 4u; k++) ((uint4 *)Bw)[64u * k + lane] = pf[k];
         const uint32_t vn = v + gridDim.x;
@@ -415,7 +414,6 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                 pf[k] = at < pn ? ln_ld16_safe(s1 + at, pn - at) : make_uint4(0, 0, 0, 0);
             }
         }
-        for (uint32_t w = lane; w < ((n + 31u) >> 5); w += 64u) bits[w] = 0u;
         if (n >= 3u) {
             for (uint32_t k = lane; k < KS_BUCKETS / 8u; k += 64u) ((uint4 *)H)[k] = make_uint4(0, 0, 0, 0);
             ln_wave_fence();
@@ -529,8 +527,6 @@ __global__ __launch_bounds__(64) void lzf_cand_mid_kernel(LzfBatch bt, LzfLaneSc
     const uint32_t n = bt.in_len[v];
     const uint8_t *src = bt.in + bt.in_off[v];
     uint16_t *cand = sc.cand + (uint64_t)v * sc.cstride;
-    uint32_t *bits = sc.bits + (uint64_t)v * sc.bstride;
-    for (uint32_t w = lane; w < ((n + 31u) >> 5); w += 64u) bits[w] = 0u;
     if (n < 3u) return;
     for (uint32_t k = lane; k < KM_BUCKETS / 4u; k += 64u) ((uint4 *)H)[k] = make_uint4(0, 0, 0, 0);
     ln_wave_fence();
@@ -673,13 +669,27 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
 
     uint32_t o = 1u, run = 0u, p = 0u; /* o, run: the reference's op and lit */
     uint32_t cb = 0xFFFFFFF0u;         /* cand entries [cb, cb+8) (+ next 8); none yet */
-    uint4 C = W, C2 = W;
+    uint4 C = W;
+#ifndef K2_NO_C2
+    uint4 C2 = W;
+#endif
     uint32_t cw = 0u, curw = 0u;       /* inserted-bitmap word of p, in flight */
     /* the last K2_RW bitmap words of the value in LDS (word w at slot w % K2_RW,
      * lane-interleaved: conflict-free), older words in the scratch array */
     __shared__ uint32_t k2_ring[K2_RW][K2_THREADS];
     uint32_t *const ring = &k2_ring[0][threadIdx.x];
 #define K2_RING(w_) ring[((w_) & (K2_RW - 1u)) * K2_THREADS]
+    /* words [0, fl) are in the scratch array: a word goes there, four at a
+     * time in one 16-byte store, before its ring slot is reused */
+    uint32_t fl = 0u;
+#define K2_FLUSH_TO(w_)                                                            \
+    do {                                                                           \
+        while (fl + K2_RW <= (w_)) {                                               \
+            *(uint4 *)(bits + fl) = make_uint4(K2_RING(fl), K2_RING(fl + 1u),      \
+                                               K2_RING(fl + 2u), K2_RING(fl + 3u)); \
+            fl += 4u;                                                              \
+        }                                                                          \
+    } while (0)
     uint32_t ms = 0u, me = 0u;         /* the last match: [ms, me) */
     uint32_t rel = 0u, q = 0u, k = 0u, lim = 0u, m = 0u;
     bool ok = true;
@@ -760,9 +770,14 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                 const uint32_t blk = p & ~7u;
                 K2_SITE(10);
                 if (blk != cb) {
+#ifdef K2_NO_C2
+                    K2_SITE(1);
+                    C = *(const uint4 *)(cand + blk);
+#else
                     if (blk == cb + 8u) K2_SITE(2); else K2_SITE(1);
                     C = blk == cb + 8u ? C2 : *(const uint4 *)(cand + blk);
                     C2 = *(const uint4 *)(cand + blk + 8u);              /* scratch has slack */
+#endif
                     cb = blk;
                 }
                 const uint32_t c = (ln_sel4(C, (p >> 1) & 3u) >> (16u * (p & 1u))) & 0xFFFFu;
@@ -780,8 +795,8 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                 word = (q > ms && q + 3u <= me) ? 0u : 0xFFFFFFFFu;         /* last match's interior */
             } else {
                 const uint32_t d = cw - (q >> 5);
-                if (d >= K2_RW) K2_SITE(3);
-                word = d == 0u ? curw : d < K2_RW ? K2_RING(q >> 5) : bits[q >> 5];
+                if (d != 0u && (q >> 5) < fl) K2_SITE(3);
+                word = d == 0u ? curw : (q >> 5) >= fl ? K2_RING(q >> 5) : bits[q >> 5];
             }
             if ((word >> (q & 31u)) & 1u) {                              /* q is the ref */
                 if (rel == 9u) K2_SITE(5);
@@ -814,7 +829,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                     K2_LITERAL(p);
                     p++;
                     if ((p & 31u) == 0u) {
-                        bits[cw] = curw;
+                        K2_FLUSH_TO(cw);
                         K2_RING(cw) = curw;
                         cw++;
                         curw = 0u;
@@ -883,11 +898,13 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                         uint32_t wo = curw, wm = 0u, wn = 0u;
                         if ((t1 >> 5) == cw) wo |= b1; else if ((t1 >> 5) == nw) wn |= b1; else wm |= b1;
                         if ((t2 >> 5) == cw) wo |= b2; else if ((t2 >> 5) == nw) wn |= b2; else wm |= b2;
-                        bits[cw] = wo;
-                        if (wm) bits[nw - 1u] = wm;
+                        K2_FLUSH_TO(cw);
                         K2_RING(cw) = wo;
                         /* words cw+1 .. nw-2 are all interior (0), nw-1 holds tails */
-                        for (uint32_t w = cw + 1u; w < nw; w++) K2_RING(w) = w + 1u == nw ? wm : 0u;
+                        for (uint32_t w = cw + 1u; w < nw; w++) {
+                            K2_FLUSH_TO(w);
+                            K2_RING(w) = w + 1u == nw ? wm : 0u;
+                        }
                         curw = wn;
                         cw = nw;
                     }
@@ -913,6 +930,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
 #undef K2_BYTE
 #undef K2_LITERAL
 #undef K2_RING
+#undef K2_FLUSH_TO
 }
 
 /* ======================================================================== */

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Ablation timing: per-kernel times for each diagnostic library build
 # (results are NOT bit-exact for ablated builds: timing only).
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/abl
 for lib in "$@"; do
     echo "== $lib"
     LZF_HIP_LIB=$PWD/gibson_amd/$lib LZF_GPU_LANE_PIPE=0 timeout -k 10 200 rocprofv3 --kernel-trace --stats \
