@@ -660,19 +660,15 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
      * store: every store instruction of the wave touches 64 lines (one
      * per lane's value), so fewer, wider stores */
     uint32_t pb0 = 0u, pb1 = 0u, pb2 = 0u, fs = 0u;
-    /* input: 16-byte window of aligned block wb (+ the next block) */
+    /* input: 16-byte window of aligned block wb */
     const uint32_t sm = (uint32_t)((uintptr_t)src & 15u);
     const uint8_t *const sa = src - sm;
-    const uint32_t last_blk = (sm + n - 1u) >> 4;
-    uint32_t wb = 0xFFFFFFF0u;          /* no block yet (wb + 1 is no block either) */
-    uint4 W = make_uint4(0, 0, 0, 0), W2 = W;
+    uint32_t wb = 0xFFFFFFF0u;          /* no block yet */
+    uint4 W = make_uint4(0, 0, 0, 0);
 
     uint32_t o = 1u, run = 0u, p = 0u; /* o, run: the reference's op and lit */
-    uint32_t cb = 0xFFFFFFF0u;         /* cand entries [cb, cb+8) (+ next 8); none yet */
+    uint32_t cb = 0xFFFFFFF0u;         /* cand entries [cb, cb+8); none yet */
     uint4 C = W;
-#ifndef K2_NO_C2
-    uint4 C2 = W;
-#endif
     uint32_t cw = 0u, curw = 0u;       /* inserted-bitmap word of p, in flight */
     /* the last K2_RW bitmap words of the value in LDS (word w at slot w % K2_RW,
      * lane-interleaved: conflict-free), older words in the scratch array */
@@ -744,8 +740,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
         const uint32_t x_ = sm + (pos_), b_ = x_ >> 4;                             \
         if (b_ != wb) {                                                            \
             K2_SITE(6);                                                            \
-            W = b_ == wb + 1u ? W2 : *(const uint4 *)(sa + 16u * b_);              \
-            if (b_ < last_blk) W2 = *(const uint4 *)(sa + 16u * (b_ + 1u));        \
+            W = *(const uint4 *)(sa + 16u * b_);   /* no prefetch: 32.6 vs 35.0 ms */ \
             wb = b_;                                                               \
         }                                                                          \
         (out_) = (ln_sel4(W, (x_ >> 2) & 3u) >> (8u * (x_ & 3u))) & 0xFFu;        \
@@ -770,14 +765,11 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                 const uint32_t blk = p & ~7u;
                 K2_SITE(10);
                 if (blk != cb) {
-#ifdef K2_NO_C2
+                    /* one 16-byte load per block entered, no prefetch of the
+                     * next: a wave load touches 64 lines, and a prefetched
+                     * block is often jumped over (34.4 vs 35.6 ms) */
                     K2_SITE(1);
                     C = *(const uint4 *)(cand + blk);
-#else
-                    if (blk == cb + 8u) K2_SITE(2); else K2_SITE(1);
-                    C = blk == cb + 8u ? C2 : *(const uint4 *)(cand + blk);
-                    C2 = *(const uint4 *)(cand + blk + 8u);              /* scratch has slack */
-#endif
                     cb = blk;
                 }
                 const uint32_t c = (ln_sel4(C, (p >> 1) & 3u) >> (16u * (p & 1u))) & 0xFFFFu;
