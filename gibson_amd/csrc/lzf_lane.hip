@@ -660,10 +660,9 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
      * store: every store instruction of the wave touches 64 lines (one
      * per lane's value), so fewer, wider stores */
     uint32_t pb0 = 0u, pb1 = 0u, pb2 = 0u, fs = 0u;
-    /* input: 16-byte window of aligned block wb */
-    const uint32_t sm = (uint32_t)((uintptr_t)src & 15u);
-    const uint8_t *const sa = src - sm;
-    uint32_t wb = 0xFFFFFFF0u;          /* no block yet */
+    /* input: the 16 bytes from position wb; loaded at the first byte that
+     * falls outside it (a literal, or a match extension's own piece) */
+    uint32_t wb = 0xFFFFFFF0u;          /* none yet */
     uint4 W = make_uint4(0, 0, 0, 0);
 
     uint32_t o = 1u, run = 0u, p = 0u; /* o, run: the reference's op and lit */
@@ -737,13 +736,14 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
     } while (0)
 #define K2_BYTE(pos_, out_)                                                        \
     do {                                                                           \
-        const uint32_t x_ = sm + (pos_), b_ = x_ >> 4;                             \
-        if (b_ != wb) {                                                            \
+        uint32_t d_ = (pos_) - wb;                                                 \
+        if (d_ >= 16u) {                                                           \
             K2_SITE(6);                                                            \
-            W = *(const uint4 *)(sa + 16u * b_);   /* no prefetch: 32.6 vs 35.0 ms */ \
-            wb = b_;                                                               \
+            W = ln_ld16_safe(src + (pos_), n - (pos_));                            \
+            wb = (pos_);                                                           \
+            d_ = 0u;                                                               \
         }                                                                          \
-        (out_) = (ln_sel4(W, (x_ >> 2) & 3u) >> (8u * (x_ & 3u))) & 0xFFu;        \
+        (out_) = (ln_sel4(W, d_ >> 2) >> (8u * (d_ & 3u))) & 0xFFu;               \
     } while (0)
 #define K2_LITERAL(pos_)                                                           \
     do {                                                                           \
@@ -847,6 +847,8 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                 K2_SITE(7);
                 const uint32_t avail = n - (p + k);
                 const uint4 a = ln_ld16_safe(src + p + k, avail), b = ln_ld16_safe(src + q + k, avail);
+                W = a;                                   /* literals after the match read it */
+                wb = p + k;
                 const uint32_t d = ln_first_diff(a, b);
                 k += d;
                 if (d < 16u) lim = k < lim ? k : lim;
