@@ -36,11 +36,11 @@ int main(int argc, char **argv)
     uint32_t bbits = argc > 4 ? (uint32_t)atoi(argv[4]) : 12;
     uint8_t *b = malloc(n + 64);
     uint32_t *tab = malloc(65536 * 4), *last = malloc(65536 * 4), *bhead = malloc(65536 * 4);
-    uint32_t *cand = malloc((size_t)n * 4), *bprev = malloc((size_t)n * 4);
+    uint32_t *cand = malloc((size_t)n * 4), *bprev = malloc((size_t)n * 4), *link = malloc((size_t)n * 4);
     uint8_t *ins = malloc(n);
     uint64_t steps = 0, lits = 0, matches = 0, walks = 0, hops = 0, maxhop = 0, mism = 0;
     uint64_t dist_hist[6] = {0}, mlen_hist[8] = {0}, backd[6] = {0};
-    uint64_t wins = 0, truncs = 0, k1hops = 0, k1max_win = 0, k1first = 0, maxsteps = 0;
+    uint64_t sk_hops = 0, sk_max_win = 0, wins = 0, truncs = 0, k1hops = 0, k1max_win = 0, k1first = 0, maxsteps = 0;
     for (uint32_t v = 0; v < count; v++) {
         syn_generate(kind, 0x5EED0002ull + kind, v, b, n);
         memset(tab, 0xFF, 65536 * 4);
@@ -49,7 +49,7 @@ int main(int argc, char **argv)
         memset(ins, 0, n);
         /* kernel 1: cand + bucket-chain hops (mix = slot*40503, bucket = top bits) */
         for (uint32_t P = 0; P + 2 < n; P += 64) {
-            uint64_t wmax = 0;
+            uint64_t wmax = 0, swmax = 0;
             for (uint32_t p = P; p < P + 64 && p + 2 < n; p++) {
                 uint32_t s = slot(b, p);
                 uint32_t m = (s * 40503u) & 0xFFFFu, bk = m >> (16 - bbits);
@@ -61,8 +61,18 @@ int main(int argc, char **argv)
                 while (e != NONE && slot(b, e) != s && p - e <= 8192) { e = bprev[e]; h++; }
                 k1hops += h;
                 if (h > wmax) wmax = h;
+                /* skip links: link(p) = latest earlier bucket position with another slot */
+                {
+                    uint32_t r = bprev[p];
+                    link[p] = r == NONE ? NONE : (slot(b, r) != s ? r : link[r]);
+                    uint32_t hs = 0, c = r;
+                    while (c != NONE && slot(b, c) != s) { c = link[c]; hs++; }
+                    sk_hops += hs;
+                    if (hs > swmax) swmax = hs;
+                }
             }
             k1max_win += wmax;
+            sk_max_win += swmax;
             k1first++;
         }
         uint32_t p = 0, vs = 0, ms = 0, me = 0;
@@ -150,6 +160,8 @@ int main(int argc, char **argv)
     for (int i = 0; i < 5; i++) printf(" %.1f", backd[i] / c);
     printf("\nkernel-1 bucket hops/position %.3f, max-over-window %.2f per 64-window\n",
            (double)k1hops / (steps ? (double)n * count : 1.0), (double)k1max_win / k1first);
+    printf("kernel-1 skip-link hops/position %.3f, max-over-window %.2f\n",
+           (double)sk_hops / ((double)n * count), (double)sk_max_win / k1first);
     printf("window parse: windows/value %.1f  truncated %.1f\n", wins / c, truncs / c);
     return 0;
 }
