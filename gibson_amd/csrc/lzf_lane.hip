@@ -427,28 +427,36 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                     act[j] = p[j] < np;
                     tri[j] = ks_rd4(Bw, act[j] ? p[j] : 0u);
                     m[j] = ln_mix(ln_slot(tri[j]));
+#ifndef KS_ABL_T
                     if (act[j]) {
                         __hip_atomic_fetch_or(&T[j][KS_T0 + ((m[j] >> 4) & 63u)], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         __hip_atomic_fetch_or(&T[j][KS_T1 + (m[j] >> 10)], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         __hip_atomic_fetch_or(&T[j][KS_T2 + (m[j] & 15u)], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
+#endif
                 }
                 ln_wave_fence();
                 unsigned long long MB[KS_WIN], MS[KS_WIN];
 #pragma unroll
                 for (uint32_t j = 0; j < KS_WIN; j++) {
+#ifdef KS_ABL_T
+                    MB[j] = MS[j] = mine;
+#else
                     MB[j] = T[j][KS_T0 + ((m[j] >> 4) & 63u)] & T[j][KS_T1 + (m[j] >> 10)];
                     MS[j] = MB[j] & T[j][KS_T2 + (m[j] & 15u)];
+#endif
                     if (!act[j]) MB[j] = MS[j] = 0ull;
                 }
                 ln_wave_fence();
 #pragma unroll
                 for (uint32_t j = 0; j < KS_WIN; j++) {
+#ifndef KS_ABL_T
                     if (act[j]) {
                         T[j][KS_T0 + ((m[j] >> 4) & 63u)] = 0ull;
                         T[j][KS_T1 + (m[j] >> 10)] = 0ull;
                         T[j][KS_T2 + (m[j] & 15u)] = 0ull;
                     }
+#endif
                 }
                 /* window j reads the heads after window j-1 wrote them (LDS
                  * ops of a wave execute in order) */
@@ -474,6 +482,9 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                     need |= cur[j] != 0u;
                 }
                 ln_wave_fence();
+#ifdef KS_ABL_WALK
+                need = false;
+#endif
                 while (__ballot(need)) {
                     need = false;
 #pragma unroll
