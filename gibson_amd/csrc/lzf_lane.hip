@@ -608,7 +608,9 @@ __global__ __launch_bounds__(64) void lzf_cand_mid_kernel(LzfBatch bt, LzfLaneSc
 /* compress, kernel 2: the greedy parse and emission, one lane per value    */
 /* ======================================================================== */
 
+#ifndef K2_THREADS
 #define K2_THREADS 256u
+#endif
 #ifndef K2_RW
 #define K2_RW      32u          /* bitmap words kept in LDS per lane (power of two) */
 #endif
