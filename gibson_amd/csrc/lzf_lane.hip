@@ -611,6 +611,9 @@ __global__ __launch_bounds__(64) void lzf_cand_mid_kernel(LzfBatch bt, LzfLaneSc
 #ifndef K2_THREADS
 #define K2_THREADS 256u
 #endif
+#ifndef K2_CB
+#define K2_CB      32u          /* cand words per parse block: 8, 16 or 32 (16 B each 8) */
+#endif
 #ifndef K2_RW
 #define K2_RW      32u          /* bitmap words kept in LDS per lane (power of two) */
 #endif
@@ -679,8 +682,10 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
     uint4 W = make_uint4(0, 0, 0, 0);
 
     uint32_t o = 1u, run = 0u, p = 0u; /* o, run: the reference's op and lit */
-    uint32_t cb = 0xFFFFFFF0u;         /* cand entries [cb, cb+8); none yet */
-    uint4 C = W;
+    /* cand words [cb, cb+32): one 64-byte, line-aligned block.  A wave load
+     * costs one line fetch per lane; the four loads of a block share it */
+    uint32_t cb = 0xFFFFFFE0u;         /* none yet (p - cb >= 32 for every p) */
+    uint4 C0 = W, C1 = W, C2 = W, C3 = W;
     uint32_t cw = 0u, curw = 0u;       /* inserted-bitmap word of p, in flight */
     /* the last K2_RW bitmap words of the value in LDS (word w at slot w % K2_RW,
      * lane-interleaved: conflict-free), older words in the scratch array */
@@ -775,17 +780,23 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
             if (p >= n - 2u) {
                 mode = K2_DONE;
             } else {
-                const uint32_t blk = p & ~7u;
+                uint32_t d = p - cb;
                 K2_SITE(10);
-                if (blk != cb) {
-                    /* one 16-byte load per block entered, no prefetch of the
-                     * next: a wave load touches 64 lines, and a prefetched
-                     * block is often jumped over (34.4 vs 35.6 ms) */
+                if (d >= K2_CB) {
                     K2_SITE(1);
-                    C = *(const uint4 *)(cand + blk);
-                    cb = blk;
+                    cb = p & ~(K2_CB - 1u);
+                    d = p - cb;
+                    const uint4 *cp = (const uint4 *)(cand + cb);
+                    C0 = cp[0];
+                    if (K2_CB >= 16u) C1 = cp[1];
+                    if (K2_CB >= 32u) {
+                        C2 = cp[2];
+                        C3 = cp[3];
+                    }
                 }
-                const uint32_t c = (ln_sel4(C, (p >> 1) & 3u) >> (16u * (p & 1u))) & 0xFFFFu;
+                const uint32_t dw = d >> 1;
+                const uint4 Cq = dw < 8u ? (dw < 4u ? C0 : C1) : (dw < 12u ? C2 : C3);
+                const uint32_t c = (ln_sel4(Cq, dw & 3u) >> (16u * (d & 1u))) & 0xFFFFu;
                 /* rel: 0 no ref; 1 ref with other bytes; 2..6 equal for rel+1
                  * bytes; 7 equal >= 8; 8 equal 3 bytes, length unknown; 9 unknown */
                 rel = c >> 13;
@@ -1245,7 +1256,9 @@ __global__ __launch_bounds__(64) void lzf_parse_wave_kernel(LzfBatch bt, LzfLane
 
 /* ---- launcher ------------------------------------------------------------ */
 
-static uint64_t lane_cstride(uint32_t max_len) { return (((uint64_t)max_len + 7u) & ~7ull) + 8u; }
+/* cand words per value: a multiple of 64 (128 bytes), so the parse's 64-byte
+ * blocks never straddle a line, plus slack for the last block */
+static uint64_t lane_cstride(uint32_t max_len) { return (((uint64_t)max_len + 63u) & ~63ull) + 64u; }
 static uint64_t lane_bstride(uint32_t max_len) { return ((((uint64_t)max_len + 31u) >> 5) + 3u) & ~3ull; }
 
 size_t lzf_lane_scratch_per_value(uint32_t max_len)
