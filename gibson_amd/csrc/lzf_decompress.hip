@@ -64,6 +64,13 @@ __device__ __forceinline__ uint32_t cd_incl_max(uint32_t x)
     return x;
 }
 
+/* J(J(i)) for a jump table J whose exits are CD_LANES (= stay) */
+__device__ __forceinline__ uint32_t cd_jump(uint32_t j)
+{
+    const uint32_t t = (uint32_t)__shfl((int)j, (int)(j & 63u));
+    return j >= 64u ? 64u : t;
+}
+
 __device__ __forceinline__ uint32_t cd_rl(uint32_t v, uint32_t l)
 {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
@@ -75,7 +82,6 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
     uint8_t *inr = smem;                               /* CD_IN_RING */
     uint8_t *outr = smem + CD_IN_RING;                 /* out_ring (power of two) */
     uint32_t *mark = (uint32_t *)(outr + out_ring);    /* 64 token-start marks */
-    uint32_t *flag = mark + CD_LANES;                  /* 64 orbit flags */
     const uint32_t imask = CD_IN_RING - 1u, omask = out_ring - 1u;
 
     const uint32_t lane = threadIdx.x;
@@ -110,19 +116,20 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
         }
 
         /* ---- 1. token boundaries -------------------------------------- */
-        const uint32_t ip = base + lane;
-        const uint32_t c = inr[ip & imask];
-        const uint32_t b1 = inr[(ip + 1u) & imask], b2 = inr[(ip + 2u) & imask];
-        const uint32_t tsz = c < 32u ? c + 2u : ((c >> 5) == 7u ? 3u : 2u);
-        uint32_t nx = lane + tsz;
-        if (ip + tsz >= in_len || nx > CD_LANES) nx = CD_LANES;   /* loop ends / next round */
+        const uint32_t ip0 = base + lane;
+        const uint32_t c0 = inr[ip0 & imask];
+        const uint32_t tsz0 = c0 < 32u ? c0 + 2u : ((c0 >> 5) == 7u ? 3u : 2u);
+        uint32_t nx = lane + tsz0;
+        if (ip0 + tsz0 >= in_len || nx > CD_LANES) nx = CD_LANES;  /* loop ends / next round */
         /* every token takes >= 2 input bytes, so a round has <= 32 tokens:
          * lane l < 32 finds the start of token l with 5 doubling levels */
+        /* every lane takes part in every shuffle: a shuffle under a partial
+         * exec mask reads nothing from the inactive source lanes */
         uint32_t J0 = nx, J1, J2, J3, J4;
-        J1 = J0 >= CD_LANES ? CD_LANES : (uint32_t)__shfl((int)J0, (int)J0);
-        J2 = J1 >= CD_LANES ? CD_LANES : (uint32_t)__shfl((int)J1, (int)J1);
-        J3 = J2 >= CD_LANES ? CD_LANES : (uint32_t)__shfl((int)J2, (int)J2);
-        J4 = J3 >= CD_LANES ? CD_LANES : (uint32_t)__shfl((int)J3, (int)J3);
+        J1 = cd_jump(J0);
+        J2 = cd_jump(J1);
+        J3 = cd_jump(J2);
+        J4 = cd_jump(J3);
         uint32_t x = 0, y;
         y = (uint32_t)__shfl((int)J0, (int)(x & 63u)); if ((lane & 1u) && x < CD_LANES) x = y;
         y = (uint32_t)__shfl((int)J1, (int)(x & 63u)); if ((lane & 2u) && x < CD_LANES) x = y;
@@ -130,13 +137,13 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
         y = (uint32_t)__shfl((int)J3, (int)(x & 63u)); if ((lane & 8u) && x < CD_LANES) x = y;
         y = (uint32_t)__shfl((int)J4, (int)(x & 63u)); if ((lane & 16u) && x < CD_LANES) x = y;
         if (lane >= 32u) x = CD_LANES;
-        flag[lane] = 0u;
-        cd_fence();
-        if (x < CD_LANES) flag[x] = 1u;
-        cd_fence();
-        const uint64_t TS = __ballot(flag[lane] != 0u);
-        const uint32_t lastT = 63u - (uint32_t)__builtin_clzll(TS);
-        const bool tok = (TS >> lane) & 1ull;
+        /* lane l now holds token l (tokens compacted in order): its bytes */
+        const bool tok = x < CD_LANES;
+        const uint32_t ntok = (uint32_t)__builtin_popcountll(__ballot(tok));
+        const uint32_t ip = base + (tok ? x : 0u);
+        const uint32_t c = inr[ip & imask];
+        const uint32_t b1 = inr[(ip + 1u) & imask], b2 = inr[(ip + 2u) & imask];
+        const uint32_t tsz = c < 32u ? c + 2u : ((c >> 5) == 7u ? 3u : 2u);
 
         /* ---- 2. decode + output offsets ------------------------------- */
         const bool lit = c < 32u;
@@ -220,7 +227,7 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
         }
         O += total;
         /* next round: the token after the last one of this round */
-        base = base + cd_rl(nx == CD_LANES ? lane + tsz : nx, lastT);
+        base = base + cd_rl(x + tsz, ntok - 1u);
     }
     if (lane == 0) {
         bt.out_len[v] = err ? 0u : O;
