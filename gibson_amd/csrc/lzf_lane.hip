@@ -479,6 +479,11 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                     q1[j] = ss ? P + 64u * j + ks_hibit(ss) + 1u : 0u;    /* pos+1 */
                     cur[j] = (act[j] && !ss) ? h : 0u;
                     if (cur[j] && (cur[j] & 15u) == id) { q1[j] = cur[j] >> 4; cur[j] = 0u; }
+                    /* the head's own link is eh, read above: the first hop is free */
+                    if (cur[j]) {
+                        cur[j] = eh;
+                        if (eh && (eh & 15u) == id) { q1[j] = eh >> 4; cur[j] = 0u; }
+                    }
                     need |= cur[j] != 0u;
                 }
                 ln_wave_fence();
