@@ -508,15 +508,12 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                     uint32_t w = 0u;
                     if (q1[j] > 1u) {                    /* q = q1 - 1 > 0 */
                         const uint32_t q = q1[j] - 1u;
-                        /* agreement of the bytes at p and q, <= 8, <= n - p */
+                        /* agreement of the bytes at p and q, <= 8, <= n - p:
+                         * both dwords read at once (one LDS round trip) */
                         const uint32_t x0 = tri[j] ^ ks_rd4(Bw, q);
-                        uint32_t k;
-                        if (x0) {
-                            k = (uint32_t)__builtin_ctz(x0) >> 3;
-                        } else {
-                            const uint32_t x1 = ks_rd4(Bw, p[j] + 4u) ^ ks_rd4(Bw, q + 4u);
-                            k = x1 ? 4u + ((uint32_t)__builtin_ctz(x1) >> 3) : 8u;
-                        }
+                        const uint32_t x1 = ks_rd4(Bw, p[j] + 4u) ^ ks_rd4(Bw, q + 4u);
+                        const uint64_t xx = ((uint64_t)x1 << 32) | x0;
+                        uint32_t k = xx ? (uint32_t)__builtin_ctzll(xx) >> 3 : 8u;
                         const uint32_t avail = n - p[j];
                         if (k > avail) k = avail;
                         w = (k1_code(k) << 13) | (p[j] - q - 1u);
