@@ -15,11 +15,11 @@
 
 #define LINES (1u << 25)            /* 4 GiB of 128-byte lines */
 
-__global__ void scattered16(const uint4 *buf, uint32_t nloads, uint32_t *out)
+__global__ void scattered16(const uint4 *buf, uint32_t nloads, uint32_t *out, uint32_t lmask)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nloads) return;
-    const uint32_t line = (i * 2654435761u) & (LINES - 1u);   /* odd multiplier: a permutation */
+    const uint32_t line = (i * 2654435761u) & lmask;          /* odd multiplier: a permutation */
     const uint4 v = buf[(uint64_t)line * 8u];                 /* 16 B at the start of the line */
     if ((v.x ^ v.y ^ v.z ^ v.w) == 0x12345678u) out[0] = i;
 }
@@ -54,7 +54,12 @@ int main()
     hipDeviceSynchronize();
     const dim3 g((nloads + 255u) / 256u), b(256);
     hipLaunchKernelGGL(coalesced16, g, b, 0, 0, buf + (size_t)LINES * 4u, nloads, out);
-    hipLaunchKernelGGL(scattered16, g, b, 0, 0, buf, nloads, out);
+    hipLaunchKernelGGL(scattered16, g, b, 0, 0, buf, nloads, out, LINES - 1u);
+    /* the same loads over 128 MiB (Infinity Cache) and 16 MiB (L2) of lines */
+    for (int rep = 0; rep < 2; rep++) {
+        hipLaunchKernelGGL(scattered16, g, b, 0, 0, buf, nloads, out, (1u << 20) - 1u);
+        hipLaunchKernelGGL(scattered16, g, b, 0, 0, buf, nloads, out, (1u << 17) - 1u);
+    }
     hipLaunchKernelGGL(scattered16_mid, g, b, 0, 0, buf, nloads, out);
     hipDeviceSynchronize();
     printf("loads per kernel %u, bytes requested %llu (16 B each)\n", nloads, (unsigned long long)nloads * 16ull);
