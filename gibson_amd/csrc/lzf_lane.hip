@@ -12,22 +12,27 @@
  *               and back-references move as unaligned 16-byte pieces.
  *
  *   compress    two kernels per batch (chunked by the scratch size):
- *     1. lzf_cand_*_kernel (one wave per value, position-parallel): for every
+ *     1. lzf_cand_small_kernel (values <= 4 KiB; lzf_cand_mid_kernel up to
+ *        64 KiB, opt-in), one wave per value, position-parallel: for every
  *        position p the nearest earlier position q with the same 16-bit slot
  *        (src/lzf_c.c:47-57, HLOG 16) -- whether or not the parse will insert
  *        q -- and how far the bytes at p and q agree (<= 8).  Packed into a
- *        u16 per position in HBM scratch ("cand").  Bucket heads in LDS are
- *        updated with ds_max_rtn in lane order, which hands every lane its
- *        bucket predecessor; a per-position chain resolves bucket collisions.
+ *        u16 per position in HBM scratch ("cand").  Same-bucket and same-slot
+ *        lanes of a window come from lane bitmaps in LDS; earlier positions
+ *        from bucket heads and per-position skip links in LDS.
  *     2. lzf_parse_lane_kernel (one lane per value): the reference's greedy
  *        parse and emission, bit-exact.  The reference's ref at p is the
  *        latest INSERTED position of p's slot (src/lzf_c.c:147-149); every
  *        position the parse visits is inserted, plus the last two positions
  *        of each match (src/lzf_c.c:227-247), so ref(p) is the first
  *        position on the cand chain from p that is not inside an earlier
- *        match.  The lane keeps an inserted-bitmap of its value (HBM
- *        scratch, the last five words in registers) and walks the chain only
- *        past skipped positions.
+ *        match.  The lane keeps an inserted-bitmap of its value (the last 32
+ *        words in LDS, older words in HBM scratch) and walks the chain only
+ *        past skipped positions.  Every wave memory instruction touches one
+ *        line per lane, so the kernel is shaped to issue few of them
+ *        (DESIGN.md §4.0).
+ *     lzf_parse_wave_kernel (opt-in): the same parse as one wave per value,
+ *        64 positions per step over LDS-resident data.
  *
  * Scratch per value: 2 B/position (cand) + 1 bit/position (bitmap).
  */
