@@ -4,15 +4,14 @@
  * Replaces src/lzf_d.c:55-149 for batches of independent streams: one
  * workgroup = one 64-lane wave per stream.  The stream is consumed in
  * rounds; a round starts at a token boundary and covers the tokens that
- * START in the next 64 input bytes:
+ * START in the next 128 input bytes (CD_ROUND):
  *
- *   1. token boundaries: every lane takes one input byte c and its token
- *      size (literal c<32: c+2 bytes; back-ref: 2, or 3 when c>>5 == 7);
- *      the chain of boundaries from lane 0 is found by pointer doubling
- *      (ds_bpermute), as in the compressor's parse orbit;
- *   2. each boundary lane decodes its token (src/lzf_d.c:66-119) and the
- *      output offsets follow from one wave prefix sum (DPP) of the token
- *      output lengths;
+ *   1. token boundaries: every lane takes two input bytes and their token
+ *      sizes (literal c<32: c+2 bytes; back-ref: 2, or 3 when c>>5 == 7);
+ *      the chain of boundaries is found by pointer doubling (ds_bpermute),
+ *      and lane l ends up holding the start of token l (<= 64 per round);
+ *   2. lane l decodes token l (src/lzf_d.c:66-119) and the output offsets
+ *      follow from one wave prefix sum (DPP) of the token output lengths;
  *   3. the reference's error checks, in its order (literal: E2BIG then
  *      EINVAL, src/lzf_d.c:72-84; back-ref: EINVAL on a truncated token,
  *      E2BIG, EINVAL on a reference before the output start,
@@ -28,6 +27,9 @@
 #include "lzf_internal.h"
 
 #define CD_LANES   64u
+#ifndef CD_ROUND
+#define CD_ROUND   128              /* input bytes whose token starts one round covers: 64 or 128 */
+#endif
 #define CD_IN_RING 4096u
 #define CD_OUT_MAX 16384u
 
@@ -102,9 +104,9 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
 
     while (first || base < in_len) {                     /* src/lzf_d.c:64, 146 */
         first = false;
-        /* stage input [base, base + 128) (tokens starting in the round and
-         * their literal payloads, <= 63 + 33 bytes) */
-        uint32_t need = base + 2u * CD_LANES;
+        /* stage input [base, base + 2 * CD_ROUND) (tokens starting in the
+         * round and their literal payloads, <= CD_ROUND - 1 + 33 bytes) */
+        uint32_t need = base + 2u * CD_ROUND;
         if (need > avail) need = avail;
         if (loaded < need) {
             uint32_t to = loaded + 2048u;
@@ -116,6 +118,41 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
         }
 
         /* ---- 1. token boundaries -------------------------------------- */
+#if CD_ROUND == 128
+        /* two input bytes per lane; jump tables J0..J5 over the round's 128
+         * positions packed two per lane (16 bits each; 128 = leaves the round).
+         * A round holds <= 64 tokens (each takes >= 2 bytes): lane l finds the
+         * start of token l with six doubling levels */
+        uint32_t PJ[6];
+        {
+            const uint32_t ipa = base + 2u * lane, ipb = ipa + 1u;
+            const uint32_t ca = inr[ipa & imask], cb = inr[ipb & imask];
+            const uint32_t ta = ca < 32u ? ca + 2u : ((ca >> 5) == 7u ? 3u : 2u);
+            const uint32_t tb = cb < 32u ? cb + 2u : ((cb >> 5) == 7u ? 3u : 2u);
+            uint32_t na = 2u * lane + ta, nb = 2u * lane + 1u + tb;
+            if (ipa + ta >= in_len || na > 128u) na = 128u;
+            if (ipb + tb >= in_len || nb > 128u) nb = 128u;
+            PJ[0] = na | (nb << 16);
+        }
+#pragma unroll
+        for (uint32_t k = 1; k < 6u; k++) {
+            const uint32_t ja = PJ[k - 1u] & 0xFFFFu, jb = PJ[k - 1u] >> 16;
+            const uint32_t wa = (uint32_t)__shfl((int)PJ[k - 1u], (int)((ja >> 1) & 63u));
+            const uint32_t wb = (uint32_t)__shfl((int)PJ[k - 1u], (int)((jb >> 1) & 63u));
+            const uint32_t va = ja >= 128u ? 128u : ((ja & 1u) ? wa >> 16 : wa & 0xFFFFu);
+            const uint32_t vb = jb >= 128u ? 128u : ((jb & 1u) ? wb >> 16 : wb & 0xFFFFu);
+            PJ[k] = va | (vb << 16);
+        }
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < 6u; b++) {
+            const uint32_t w = (uint32_t)__shfl((int)PJ[b], (int)((x >> 1) & 63u));
+            const uint32_t y = (x & 1u) ? w >> 16 : w & 0xFFFFu;
+            if (((lane >> b) & 1u) && x < 128u) x = y;
+        }
+        /* lane l now holds token l (tokens compacted in order): its bytes */
+        const bool tok = x < 128u;
+#else
         const uint32_t ip0 = base + lane;
         const uint32_t c0 = inr[ip0 & imask];
         const uint32_t tsz0 = c0 < 32u ? c0 + 2u : ((c0 >> 5) == 7u ? 3u : 2u);
@@ -139,6 +176,7 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
         if (lane >= 32u) x = CD_LANES;
         /* lane l now holds token l (tokens compacted in order): its bytes */
         const bool tok = x < CD_LANES;
+#endif
         const uint32_t ntok = (uint32_t)__builtin_popcountll(__ballot(tok));
         const uint32_t ip = base + (tok ? x : 0u);
         const uint32_t c = inr[ip & imask];
