@@ -135,14 +135,26 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s)
     return e;
 }
 
+/* smallest batch the lane generation takes (LZF_GPU_LANE_MIN overrides) */
+uint32_t lane_min_count()
+{
+    const char *e = getenv("LZF_GPU_LANE_MIN");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : 163840u;
+}
+
 hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
 {
     switch (kernel_gen()) {
     case GEN_SERIAL: return lzf_launch_compress_serial(b, s);
     case GEN_WINDOW: return lzf_launch_compress(b, s);
     default:
-        /* batches with values past 4 KiB go to the window generation */
-        return lzf_lane_compress_supported(b.max_len) ? lane_compress(b, s) : lzf_launch_compress(b, s);
+        /* batches with values past 4 KiB, and small batches, go to the window
+         * generation: the lane parse runs one value per lane, so its time has a
+         * floor of one whole value's parse (~5 ms); below ~160 k values one
+         * wave per value finishes first (tools/crossover.py) */
+        return (lzf_lane_compress_supported(b.max_len) && b.count >= lane_min_count())
+                   ? lane_compress(b, s)
+                   : lzf_launch_compress(b, s);
     }
 }
 
@@ -441,7 +453,8 @@ const char *lzf_gpu_kernel_info(void)
             lzf_decompress_kernel_name();
         break;
     default:
-        s = std::string("compress=lane(cand+parse; window64 past 4 KiB) decompress=") +
+        s = std::string("compress=lane(cand+parse; window64 past 4 KiB or below ") +
+            std::to_string(lane_min_count()) + " values) decompress=" +
             (lane_decoder() ? "lane" : lzf_decompress_kernel_name());
         break;
     }

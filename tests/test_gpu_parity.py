@@ -20,6 +20,14 @@ pytestmark = pytest.mark.gpu
 GENERATIONS = ["lane", "window", "serial"]
 
 
+@pytest.fixture(autouse=True)
+def _lane_for_any_batch(monkeypatch):
+    # the library routes batches below LZF_GPU_LANE_MIN values to the window
+    # generation (faster there); the parity batches here are small, so the
+    # lane kernels are asked for explicitly
+    monkeypatch.setenv("LZF_GPU_LANE_MIN", "0")
+
+
 @pytest.fixture(params=GENERATIONS)
 def generation(request, monkeypatch):
     if request.param == "lane":
@@ -179,6 +187,18 @@ def test_wave_parse(oracle, monkeypatch, align):
     vals += [synth(k, 0x5EED00E1, n, n) for k in range(6) for n in (1, 2, 3, 4, 5, 63, 64, 65, 66, 67, 130)]
     caps = [rnd.choice([max(1, len(v) - 4), len(v) + len(v) // 16 + 64, rnd.randint(1, len(v) + 8)]) for v in vals]
     assert gpu_compress(vals, caps, align=align) == [oracle.compress(v, c) for v, c in zip(vals, caps)]
+
+
+def test_small_batch_routing(oracle, monkeypatch):
+    # default threshold: a small batch compresses with the window generation,
+    # bit-exact like the rest
+    from tests.gpu_batch import gpu_compress
+    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.delenv("LZF_GPU_LANE_MIN", raising=False)
+    rnd = random.Random(5)
+    vals = [synth(rnd.randrange(6), 0x5EED00C0, i, rnd.randint(1, 4096)) for i in range(200)]
+    caps = [max(1, len(v) - 4) for v in vals]
+    assert gpu_compress(vals, caps) == [oracle.compress(v, c) for v, c in zip(vals, caps)]
 
 
 def test_lane_order_repair_path(oracle, monkeypatch):
