@@ -426,11 +426,15 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
             for (uint32_t P = 0; P < np; P += 64u * KS_WIN) {
                 uint32_t p[KS_WIN], m[KS_WIN], tri[KS_WIN];
                 bool act[KS_WIN];
+                /* the step's byte reads first, in one LDS round trip */
 #pragma unroll
                 for (uint32_t j = 0; j < KS_WIN; j++) {
                     p[j] = P + 64u * j + lane;
                     act[j] = p[j] < np;
                     tri[j] = ks_rd4(Bw, act[j] ? p[j] : 0u);
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < KS_WIN; j++) {
                     m[j] = ln_mix(ln_slot(tri[j]));
 #ifndef KS_ABL_T
                     if (act[j]) {
