@@ -17,7 +17,7 @@
  *      E2BIG, EINVAL on a reference before the output start,
  *      src/lzf_d.c:100-131) -- the first failing token decides errno;
  *   4. the output bytes are produced 64 at a time, one per lane: the owning
- *      token comes from a max-scan of token-start marks, the byte from the
+ *      token comes from a ballot of token-start marks, the byte from the
  *      LDS input ring (literal) or the LDS output window (back-ref); a
  *      back-ref byte whose source lies in the same 64-byte group (runs,
  *      src/lzf_d.c:137-142 copies byte-serially so overlap replicates) is
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t *inr = smem;                               /* CD_IN_RING */
     uint8_t *outr = smem + CD_IN_RING;                 /* out_ring (power of two) */
-    uint32_t *mark = (uint32_t *)(outr + out_ring);    /* 64 token-start marks */
+    uint32_t *mark = (uint32_t *)(outr + out_ring);    /* 64 token-start marks (group tags) */
     const uint32_t imask = CD_IN_RING - 1u, omask = out_ring - 1u;
 
     const uint32_t lane = threadIdx.x;
@@ -96,6 +96,7 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
     /* as the reference, a 0-length stream still reads its first control byte */
     const uint32_t avail = in_len ? in_len : 1u;
 
+    mark[lane] = 0u;            /* group tags are >= 1 */
     uint32_t loaded = 0;
     uint32_t base = 0;          /* input offset of the round's first token */
     uint32_t O = 0;             /* output bytes produced so far */
@@ -222,20 +223,26 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
         const uint32_t total = cd_rl(incl, 63u);           /* round output bytes */
 
         /* ---- 4. output bytes, 64 per step ------------------------------ */
-        uint32_t carry = 0;          /* token lane owning the first byte of the group */
+        /* tokens sit in lanes in output order, so the owner of output byte b
+         * of a group is (tokens started before the group) + (token starts in
+         * the group at or below b) - 1: the starts are marked in LDS with the
+         * group's tag (gb + 1, never reused, so the marks need no clearing)
+         * and read back as one ballot */
+        uint32_t tbase = 0;          /* tokens started before the group */
 #ifdef LZF_CD_ABLATE_OUTPUT           /* diagnostic builds only: time discovery alone */
         for (uint32_t g = 0; g < 0u; g += CD_LANES) {
 #else
         for (uint32_t g = 0; g < total; g += CD_LANES) {
 #endif
             const uint32_t gb = O + g;                     /* group's first output offset */
-            mark[lane] = 0u;
+            if (tok && Ot >= gb && Ot < gb + CD_LANES) mark[Ot - gb] = gb + 1u;
             cd_fence();
-            if (tok && Ot >= gb && Ot < gb + CD_LANES) mark[Ot - gb] = lane + 1u;
-            cd_fence();
-            uint32_t k = cd_incl_max(mark[lane]);
-            k = k ? k - 1u : carry;
-            carry = cd_rl(k, 63u);
+            const uint64_t S = __ballot(mark[lane] == gb + 1u);
+            const uint32_t le = __builtin_amdgcn_mbcnt_hi((uint32_t)(S >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)S, 0u)) +
+                                (uint32_t)((S >> lane) & 1ull);
+            const uint32_t k = tbase + le - 1u;
+            tbase += (uint32_t)__builtin_popcountll(S);
             const uint32_t o = gb + lane;
             const bool live = g + lane < total;
             const uint32_t tInf = (uint32_t)__shfl((int)tinfo, (int)k);
