@@ -21,6 +21,8 @@
 
 #include <mutex>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "lzf_internal.h"
 #include "../../include/lzf.h"
@@ -227,11 +229,23 @@ struct Meta {               /* one value's descriptor, packed for one copy */
     int32_t err;
 };
 
+/* One stage of the chunked host pipeline: its own stream, pinned and device
+ * buffers, and the chunk it holds until the results are copied out. */
+struct Slot {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    Buf d_in, d_out, d_meta;
+    Buf h_in{nullptr, 0, true}, h_out{nullptr, 0, true}, h_meta{nullptr, 0, true};
+    uint32_t first = 0, count = 0;
+    bool busy = false;
+};
+
 struct Ctx {
     int dev = 0;
     hipStream_t stream = nullptr;
     Buf d_in, d_out, d_meta;
     Buf h_in{nullptr, 0, true}, h_out{nullptr, 0, true}, h_meta{nullptr, 0, true};
+    Slot slot[2];
     Ctx()
     {
         const char *e = getenv("LZF_GPU_DEVICE");
@@ -259,6 +273,141 @@ void check(hipError_t e, const char *what)
     if (e != hipSuccess) die(what, e);
 }
 
+/* Run f(lo, hi) over [0, n) split into up to `threads` ranges. */
+template <class F> void parallel_ranges(uint32_t n, uint32_t threads, F f)
+{
+    if (threads <= 1 || n < 2u * threads) {
+        f(0u, n);
+        return;
+    }
+    std::vector<std::thread> ts;
+    const uint32_t per = (n + threads - 1u) / threads;
+    for (uint32_t t = 1; t < threads; t++) {
+        const uint32_t lo = t * per, hi = lo + per < n ? lo + per : n;
+        if (lo < hi) ts.emplace_back([=]() { f(lo, hi); });
+    }
+    f(0u, per < n ? per : n);
+    for (auto &t : ts) t.join();
+}
+
+uint32_t host_threads()
+{
+    const char *e = getenv("LZF_GPU_HOST_THREADS");
+    if (e) return (uint32_t)atoi(e) > 0 ? (uint32_t)atoi(e) : 1u;
+    const unsigned hc = std::thread::hardware_concurrency();
+    return hc >= 8u ? 8u : (hc ? hc : 1u);
+}
+
+/* Large host batches: values in chunks through two slots on two streams.
+ * The CPU gathers chunk k+1's values (several threads) while chunk k moves
+ * over PCIe and runs; results are scattered back once a slot comes round
+ * again.  Each chunk's values are packed (inputs back to back, outputs at
+ * their caps back to back), so only their bytes cross the bus. */
+int host_batch_pipelined(bool compress, const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                         uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len,
+                         int32_t *err, uint32_t count, uint64_t chunk_in, uint64_t chunk_out)
+{
+    Ctx &c = ctx();
+    DeviceGuard g(c.dev);
+    const uint32_t threads = host_threads();
+    for (auto &sl : c.slot) {
+        if (!sl.stream) check(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking), "hipStreamCreate");
+        if (!sl.done) check(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming), "hipEventCreate");
+        sl.busy = false;
+    }
+    const size_t mrec = 2 * sizeof(uint64_t) + 3 * sizeof(uint32_t) + sizeof(int32_t);
+    /* results of a finished slot back to the caller's arrays */
+    auto drain = [&](Slot &sl) {
+        if (!sl.busy) return;
+        check(hipEventSynchronize(sl.done), "hipEventSynchronize");
+        const uint32_t n = sl.count;
+        const uint64_t *m_out_off = (const uint64_t *)sl.h_meta.p + n;
+        const uint32_t *m_out_len = (const uint32_t *)(m_out_off + n) + 2u * n;
+        const int32_t *m_err = (const int32_t *)(m_out_len + n);
+        const uint8_t *h_out = (const uint8_t *)sl.h_out.p;
+        parallel_ranges(n, threads, [&](uint32_t lo, uint32_t hi) {
+            for (uint32_t k = lo; k < hi; k++) {
+                const uint32_t i = sl.first + k;
+                out_len[i] = m_out_len[k];
+                if (err) err[i] = m_err[k];
+                if (m_out_len[k]) memcpy(out + out_off[i], h_out + m_out_off[k], m_out_len[k]);
+            }
+        });
+        sl.busy = false;
+    };
+    uint32_t i0 = 0, k = 0;
+    while (i0 < count) {
+        /* the chunk: values [i0, i1) */
+        uint64_t bin = 0, bout = 0;
+        uint32_t i1 = i0, max_len = 0;
+        while (i1 < count) {
+            const uint64_t li = in_len[i1] ? in_len[i1] : 1u;     /* a 0-length stream reads 1 byte */
+            if (i1 > i0 && (bin + li > chunk_in || bout + out_cap[i1] > chunk_out)) break;
+            bin += li;
+            bout += out_cap[i1];
+            const uint32_t l = compress ? in_len[i1] : out_cap[i1];
+            if (l > max_len) max_len = l;
+            i1++;
+        }
+        Slot &sl = c.slot[k & 1u];
+        drain(sl);
+        const uint32_t n = i1 - i0;
+        uint8_t *h_in = (uint8_t *)sl.h_in.get(bin);
+        uint8_t *h_meta = (uint8_t *)sl.h_meta.get((size_t)n * mrec);
+        uint8_t *d_in = (uint8_t *)sl.d_in.get(bin);
+        uint8_t *d_out = (uint8_t *)sl.d_out.get(bout);
+        uint8_t *d_meta = (uint8_t *)sl.d_meta.get((size_t)n * mrec);
+        sl.h_out.get(bout);
+        uint64_t *m_in_off = (uint64_t *)h_meta, *m_out_off = m_in_off + n;
+        uint32_t *m_in_len = (uint32_t *)(m_out_off + n), *m_out_cap = m_in_len + n;
+        {
+            uint64_t a = 0, b = 0;
+            for (uint32_t j = 0; j < n; j++) {
+                const uint32_t i = i0 + j;
+                m_in_off[j] = a;
+                m_out_off[j] = b;
+                m_in_len[j] = in_len[i];
+                m_out_cap[j] = out_cap[i];
+                a += in_len[i] ? in_len[i] : 1u;
+                b += out_cap[i];
+            }
+        }
+        parallel_ranges(n, threads, [&](uint32_t lo, uint32_t hi) {
+            for (uint32_t j = lo; j < hi; j++) {
+                const uint32_t i = i0 + j;
+                memcpy(h_in + m_in_off[j], in + in_off[i], in_len[i] ? in_len[i] : 1u);
+            }
+        });
+        const size_t res_off = (uint8_t *)(m_out_cap + n) - h_meta;
+        check(hipMemcpyAsync(d_in, h_in, bin, hipMemcpyHostToDevice, sl.stream), "hipMemcpyAsync");
+        check(hipMemcpyAsync(d_meta, h_meta, res_off, hipMemcpyHostToDevice, sl.stream), "hipMemcpyAsync");
+        LzfBatch b{};
+        b.in = d_in;
+        b.in_off = (const uint64_t *)d_meta;
+        b.out_off = b.in_off + n;
+        b.in_len = (const uint32_t *)(b.out_off + n);
+        b.out_cap = b.in_len + n;
+        b.out_len = (uint32_t *)(b.out_cap + n);
+        b.err = (int32_t *)(b.out_len + n);
+        b.out = d_out;
+        b.count = n;
+        b.max_len = max_len;
+        check(compress ? launch_compress(b, sl.stream) : launch_decompress(b, sl.stream), "kernel launch");
+        check(hipMemcpyAsync(h_meta + res_off, d_meta + res_off, (size_t)n * mrec - res_off,
+                             hipMemcpyDeviceToHost, sl.stream), "hipMemcpyAsync");
+        check(hipMemcpyAsync(sl.h_out.p, d_out, bout, hipMemcpyDeviceToHost, sl.stream), "hipMemcpyAsync");
+        check(hipEventRecord(sl.done, sl.stream), "hipEventRecord");
+        sl.first = i0;
+        sl.count = n;
+        sl.busy = true;
+        i0 = i1;
+        k++;
+    }
+    drain(c.slot[k & 1u]);
+    drain(c.slot[(k + 1u) & 1u]);
+    return LZF_GPU_OK;
+}
+
 /* Host batch: stage arena + descriptors, run, copy back. */
 int host_batch(bool compress, const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
                uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len,
@@ -266,6 +415,20 @@ int host_batch(bool compress, const uint8_t *in, const uint64_t *in_off, const u
 {
     if (!count || !in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len)
         return LZF_GPU_EARG;
+    {
+        /* large batches whose outputs are not much bigger than their inputs
+         * (compress, or decompress with caps near the values' sizes) go
+         * through the chunked pipeline */
+        uint64_t sin = 0, sout = 0;
+        for (uint32_t i = 0; i < count; i++) {
+            sin += in_len[i] ? in_len[i] : 1u;
+            sout += out_cap[i];
+        }
+        const uint64_t chunk = 32ull << 20;
+        if (sin >= 2 * chunk && sout <= 4 * sin)
+            return host_batch_pipelined(compress, in, in_off, in_len, out, out_off, out_cap, out_len, err,
+                                        count, chunk, 4 * chunk);
+    }
     Ctx &c = ctx();
     DeviceGuard g(c.dev);
     uint64_t in_end = 0, out_end = 0;

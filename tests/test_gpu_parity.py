@@ -340,6 +340,45 @@ def test_full_size_roundtrip(kind, seed, n, count, oracle):
         assert got == exp, (kind, n, i)
 
 
+def test_host_batch_pipelined(oracle):
+    # a host batch of 96 MiB runs the chunked two-slot pipeline: values in
+    # shuffled, unaligned arena order with mixed sizes, checked against the
+    # oracle (a sample) and by the round trip (all)
+    import gibson_amd
+    rnd = random.Random(17)
+    count = 24000
+    sizes = [rnd.choice([4096, 4096, 4096, rnd.randint(1, 8192)]) for _ in range(count)]
+    order = list(range(count))
+    rnd.shuffle(order)
+    pos, offs = 0, [0] * count
+    for i in order:
+        offs[i] = pos
+        pos += sizes[i] + rnd.randint(0, 3)
+    arena = np.zeros(pos + 16, np.uint8)
+    kinds = [rnd.randrange(6) for _ in range(count)]
+    for i in range(count):
+        arena[offs[i]:offs[i] + sizes[i]] = np.frombuffer(synth(kinds[i], 0x5EED00B0, i, sizes[i]), np.uint8)
+    off = np.array(offs, dtype=np.uint64)
+    ln = np.array(sizes, dtype=np.uint32)
+    cap = np.maximum(ln.astype(np.int64) - 4, 1).astype(np.uint32)
+    out = np.zeros_like(arena)
+    olen = np.zeros(count, np.uint32)
+    gibson_amd.host_compress_batch(arena, off, ln, out, off, cap, olen)
+    for i in rnd.sample(range(count), 400):
+        v = bytes(arena[offs[i]:offs[i] + sizes[i]])
+        exp = oracle.compress(v, int(cap[i]))
+        got = bytes(out[offs[i]:offs[i] + olen[i]]) if olen[i] else None
+        assert got == exp, i
+    ok = olen > 0
+    dec = np.zeros_like(arena)
+    dl = np.zeros(int(ok.sum()), np.uint32)
+    er = np.zeros(int(ok.sum()), np.int32)
+    gibson_amd.host_decompress_batch(out, off[ok], olen[ok], dec, off[ok], ln[ok], dl, er)
+    assert (dl == ln[ok]).all() and (er == 0).all()
+    for i in np.nonzero(ok)[0][:2000]:
+        assert bytes(dec[offs[i]:offs[i] + sizes[i]]) == bytes(arena[offs[i]:offs[i] + sizes[i]])
+
+
 def test_host_batch_api(oracle):
     import gibson_amd
     vals = [synth(1, 11, i, 4096) for i in range(64)] + [synth(4, 11, 0, 4096)]
