@@ -57,7 +57,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="json4k", choices=sorted(WORKLOADS))
+    ap.add_argument("--mode", default="roundtrip", choices=("roundtrip", "decompress"),
+                    help="roundtrip = the headline (compress+decompress); decompress = "
+                         "BASELINE configs[3], decode of pre-compressed blocks only")
+    ap.add_argument("--workload", default="", choices=[""] + sorted(WORKLOADS),
+                    help="default: json4k (roundtrip), text8k (decompress)")
     ap.add_argument("--count", type=int, default=0, help="values per GPU (default: workload's)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-count", type=int, default=0, help="CPU baseline sample values")
@@ -65,7 +69,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(kind, seed, n, count, threads):
+def cpu_baseline(kind, seed, n, count, threads, decode_only=False):
     """Time the CPU codec on a bounded sample (checker/baseline only)."""
     ref = os.path.join(ROOT, "oracle", "_ref", "cpu_bench_ref")
     port = os.path.join(ROOT, "oracle", "cpu_bench")
@@ -78,12 +82,12 @@ def cpu_baseline(kind, seed, n, count, threads):
         return {"error": out.stderr.strip()[-200:]}
     r = json.loads(out.stdout)
     return {
-        "value": round(r["roundtrip_GBps"], 4),
+        "value": round(r["decompress_GBps" if decode_only else "roundtrip_GBps"], 4),
         "unit": "GB/s",
         "cores": threads,
         "kind": r["kind"],
         "sample": f"{count} values x {n} B (first {count} of the workload's value indices), "
-                  f"compress+decompress, median of 5 after 1 warm-up, one value per OpenMP "
+                  f"{'decompress of the reference-compressed values' if decode_only else 'compress+decompress'}, median of 5 after 1 warm-up, one value per OpenMP "
                   f"thread; compress {r['compress_GBps']:.3f} GB/s, decompress "
                   f"{r['decompress_GBps']:.3f} GB/s, ratio {r['comp_bytes'] / r['in_bytes']:.4f}",
         "cpu": _cpu_model(),
@@ -123,9 +127,15 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    if not a.workload:
+        a.workload = "text8k" if a.mode == "decompress" else "json4k"
     cfg_idx, kind, seed, n, count = WORKLOADS[a.workload]
+    if a.mode == "decompress" and a.workload == "text8k":
+        count = 8 << 20                                  # BASELINE configs[3]: 8 M blocks
     if a.count:
         count = a.count
+    if a.mode == "decompress":
+        return main_decompress(a, world, rank, dev, cfg_idx, kind, seed, n, count)
 
     # ---- data in HBM: value i of this rank is global value rank + k*world ----
     src = torch.empty(count * n, dtype=torch.uint8, device=dev)
@@ -244,6 +254,127 @@ def main():
             threads = a.cpu_threads or min(16, os.cpu_count() or 1)
             cnt = a.cpu_count or min(count, max(64, (4 << 30) // n))
             line["cpu_baseline"] = cpu_baseline(kind, seed, n, cnt, threads)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main_decompress(a, world, rank, dev, cfg_idx, kind, seed, n, count):
+    """BASELINE configs[3]: decode-path throughput.  Setup (untimed): values
+    are generated and compressed (out_len = n-4) in chunks of 1 M, into slots
+    of n bytes; the generator buffer is then freed.  A step is one
+    lzf_gpu_decompress_batch over all `count` streams with out_len = n.
+    Values that did not compress (clen == 0) would decode a 0-length stream
+    and fail at once; they are excluded from the bytes counted."""
+    chunk = min(count, 1 << 20)
+    first, stride = shard(rank, world)
+    off = torch.arange(count, dtype=torch.int64, device=dev) * n
+    comp = torch.empty(count * n, dtype=torch.uint8, device=dev)
+    clen = torch.zeros(count, dtype=torch.int32, device=dev)
+    src = torch.empty(chunk * n, dtype=torch.uint8, device=dev)
+    coff = torch.arange(chunk, dtype=torch.int64, device=dev) * n
+    cin = torch.full((chunk,), n, dtype=torch.int32, device=dev)
+    ccap = torch.full((chunk,), n - 4, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream()
+    for c0 in range(0, count, chunk):
+        m = min(chunk, count - c0)
+        gibson_amd.synth_fill(kind, seed, first + c0 * stride, stride, m, n, src)
+        gibson_amd.compress_batch(src, coff[:m], cin[:m], comp[c0 * n:], coff[:m], ccap[:m],
+                                  clen[c0:c0 + m], n, stream)
+    torch.cuda.synchronize()
+    dcap = torch.full((count,), n, dtype=torch.int32, device=dev)
+    dec = torch.empty(count * n, dtype=torch.uint8, device=dev)
+    dlen = torch.zeros(count, dtype=torch.int32, device=dev)
+    derr = torch.zeros(count, dtype=torch.int32, device=dev)
+    ev = []
+
+    def step(record):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        gibson_amd.decompress_batch(comp, off, clen, dec, off, dcap, dlen, derr, n, stream)
+        e1.record(stream)
+        if record:
+            ev.append((e0, e1))
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    t_dec = sum(e0.elapsed_time(e1) for e0, e1 in ev) / a.steps / 1e3
+
+    # sanity (outside the timed region): every compressed value decodes back
+    ok = clen > 0
+    n_ok = int(ok.sum())
+    c_bytes = int(clen.to(torch.int64).sum())
+    good = bool(((dlen == n) | ~ok).all()) and not bool((derr[ok] != 0).any())
+    for c0 in range(0, count, chunk):
+        m = min(chunk, count - c0)
+        gibson_amd.synth_fill(kind, seed, first + c0 * stride, stride, m, n, src)
+        diff = (dec[c0 * n:(c0 + m) * n].view(m, n) != src[:m * n].view(m, n)).any(dim=1)
+        good = good and not bool((diff & ok[c0:c0 + m]).any())
+    del src
+
+    (wall, t_dec), (n_ok_all, c_bytes_all, bad_ranks) = reduce_stats(
+        [wall, t_dec], [n_ok, c_bytes, 0 if good else 1], device=dev)
+    if rank == 0:
+        sec_per_step = wall / a.steps
+        out_bytes_all = n_ok_all * n
+        dec_bytes = c_bytes + n_ok * n                          # read C, write N (this rank)
+        ach = dec_bytes / t_dec / 1e9
+        line = {
+            "metric": "LZF GB/s (device-resident) decompress-only over pre-compressed value blocks",
+            "value": round(out_bytes_all / sec_per_step / 1e9, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(sec_per_step * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{count // (1 << 20)}M x {n // 1024} KiB pre-compressed blocks per GPU, "
+                            f"decompress only (BASELINE configs[3])" if count >= (1 << 20) else
+                            f"{count} x {n} B pre-compressed blocks per GPU, decompress only",
+                "baseline_config": 3,
+                "values_per_gpu": count,
+                "value_bytes": n,
+                "out_len_policy": f"compressed at n-4 (src/query.c:385), decoded with out_len = {n}",
+                "sharding": "round-robin value i -> rank i mod N, no collective",
+                "compressed_fraction": round(n_ok_all / (count * world), 4),
+                "ratio": round(c_bytes_all / max(1.0, out_bytes_all), 4),
+                "kernels": gibson_amd.kernel_info(),
+                "roundtrip_ok": bad_ranks == 0,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "lzf_decompress",
+                "achieved": round(ach, 2),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBPS, 5),
+                "traffic": _traffic(f"{a.workload}_decode", "lzf_decompress", count),
+                "algorithmic_bytes": dec_bytes,
+                "per_kernel_ms": {"lzf_decompress": round(t_dec * 1e3, 3)},
+            },
+        }
+        if world == 1 and not a.no_cpu:
+            threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+            cnt = a.cpu_count or min(count, max(64, (4 << 30) // n))
+            line["cpu_baseline"] = cpu_baseline(kind, seed, n, cnt, threads, decode_only=True)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
