@@ -150,7 +150,7 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
     case GEN_SERIAL: return lzf_launch_compress_serial(b, s);
     case GEN_WINDOW: return lzf_launch_compress(b, s);
     default:
-        /* batches with values past 4 KiB, and small batches, go to the window
+        /* batches with values past 8 KiB, and small batches, go to the window
          * generation: the lane parse runs one value per lane, so its time has a
          * floor of one whole value's parse (~5 ms); below ~160 k values one
          * wave per value finishes first (tools/crossover.py) */
@@ -616,7 +616,7 @@ const char *lzf_gpu_kernel_info(void)
             lzf_decompress_kernel_name();
         break;
     default:
-        s = std::string("compress=lane(cand+parse; window64 past 4 KiB or below ") +
+        s = std::string("compress=lane(cand+parse; window64 past 8 KiB or below ") +
             std::to_string(lane_min_count()) + " values) decompress=" +
             (lane_decoder() ? "lane" : lzf_decompress_kernel_name());
         break;

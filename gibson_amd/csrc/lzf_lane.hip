@@ -12,8 +12,8 @@
  *               and back-references move as unaligned 16-byte pieces.
  *
  *   compress    two kernels per batch (chunked by the scratch size):
- *     1. lzf_cand_small_kernel (values <= 4 KiB; lzf_cand_mid_kernel up to
- *        64 KiB, opt-in), one wave per value, position-parallel: for every
+ *     1. lzf_cand_small_kernel (values <= 4 KiB, and <= 8 KiB with a 3-bit
+ *        identity; lzf_cand_mid_kernel up to 64 KiB, opt-in), one wave per value, position-parallel: for every
  *        position p the nearest earlier position q with the same 16-bit slot
  *        (src/lzf_c.c:47-57, HLOG 16) -- whether or not the parse will insert
  *        q -- and how far the bytes at p and q agree (<= 8).  Packed into a
@@ -281,8 +281,8 @@ hipError_t lzf_launch_decompress_lane(const LzfBatch &b, hipStream_t s)
 #ifndef KS_WIN
 #define KS_WIN      2u            /* small class: windows per step (2: 31.4 ms, 1: 33.1, 3: 36.9, 4: 36.3 on json4k) */
 #endif
-#define KS_BUCKETS  4096u         /* small class: 12-bit bucket, 4-bit identity */
-#define KS_MAXN     4096u         /* staged whole; positions + 1 fit 12 bits */
+#define KS_MAXN     4096u         /* small class: 12-bit bucket, 4-bit identity, positions + 1 fit 12 bits */
+#define KS8_MAXN    8192u         /* small class, 8 KiB: 13-bit bucket, 3-bit identity, positions + 1 fit 13 bits */
 #define KM_BUCKETS  2048u         /* mid class */
 #define KM_MAXN     65536u        /* positions + 1 fit 16 bits */
 
@@ -352,21 +352,25 @@ __device__ __noinline__ void k1_fix_order(uint32_t (&r)[K1_WIN], const uint32_t 
         if (act[j]) r[j] = fixed[j];
 }
 
-/* Small class (every value <= KS_MAXN bytes: all positions inside one 8 KiB
- * window).  Persistent workgroups of one wave walk the batch; the next
+/* Small class (every value <= MAXN <= 8 KiB bytes: all positions inside one
+ * 8 KiB window, so no window test).  Persistent workgroups of one wave walk the batch; the next
  * value's bytes are loaded into registers while the current one is
  * processed and then staged in LDS, so the position loop reads only LDS.
  *
- * Slot-mix m = mix(slot) (bijective): bucket = m >> 4, identity = m & 15.
+ * Slot-mix m = mix(slot) (bijective): bucket = m >> IDB, identity = the low
+ * IDB bits (IDB = 4 for values <= 4 KiB, 3 for values <= 8 KiB, so that an
+ * entry [pos+1 | identity] fits 16 bits).
  * Per window of 64 positions, lanes with the same bucket / the same slot are
- * found exactly with lane bitmaps keyed by m's digits [4,10), [10,16) and
- * [0,4) (ds_or_b64, AND of the read-backs).  Per position the kernel keeps,
+ * found exactly with lane bitmaps keyed by m's digits [IDB,IDB+6),
+ * [IDB+6,16) and [0,IDB) (ds_or_b64, AND of the read-backs).  Per position the kernel keeps,
  * in LDS, the bucket head (latest position of the bucket) and a skip link:
  * the latest earlier position of the bucket with ANOTHER identity.  The
  * same-slot predecessor is then the nearest same-slot lane below, else found
  * from the head by following skip links until the identity matches (one hop
- * per change of identity, not per position).  Entries are [pos+1:12 |
- * identity:4].  LDS: heads 8 KiB, links 8 KiB, bytes 4 KiB, bitmaps 1.1 KiB per window. */
+ * per change of identity, not per position).  Entries are [pos+1:16-IDB |
+ * identity:IDB].  LDS at 4 KiB: heads 8 KiB, links 8 KiB, bytes 4 KiB,
+ * bitmaps 1.1 KiB per window; at 8 KiB: heads 16 KiB, links 16 KiB, bytes
+ * 8 KiB, bitmaps 1.6 KiB per window. */
 __device__ __forceinline__ uint32_t ks_rd4(const uint32_t *w, uint32_t x)
 {
     return __builtin_amdgcn_alignbyte(w[(x >> 2) + 1u], w[x >> 2], x & 3u);
@@ -378,28 +382,31 @@ __device__ __forceinline__ uint32_t ks_hibit(uint64_t m)
     return 63u - (uint32_t)__builtin_clzll(m);
 }
 
-#define KS_T0 0u      /* digit m[4,10)  : 64 entries */
-#define KS_T1 64u     /* digit m[10,16) : 64 entries */
-#define KS_T2 128u    /* digit m[0,4)   : 16 entries */
-#define KS_TN 144u
-
+template <uint32_t IDB, uint32_t MAXN>
 __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLaneScratch sc)
 {
-    __shared__ __attribute__((aligned(16))) uint16_t H[KS_BUCKETS];
-    __shared__ uint16_t E[KS_MAXN];
-    __shared__ __attribute__((aligned(16))) uint32_t Bw[KS_MAXN / 4u + 4u];
-    __shared__ unsigned long long T[KS_WIN][KS_TN];
+    static_assert(MAXN <= LZF_WINDOW && ((MAXN - 1u) >> (16u - IDB)) == 0u, "entry [pos+1 | id] must fit 16 bits");
+    constexpr uint32_t BUCKETS = 1u << (16u - IDB), IDM = (1u << IDB) - 1u;
+    constexpr uint32_t T0 = 0u;                          /* digit m[IDB, IDB+6)  : 64 entries */
+    constexpr uint32_t T1 = 64u;                         /* digit m[IDB+6, 16)   : 2^(10-IDB) entries */
+    constexpr uint32_t T2 = T1 + (1u << (10u - IDB));    /* digit m[0, IDB)      : 2^IDB entries */
+    constexpr uint32_t TN = T2 + (1u << IDB);
+    constexpr uint32_t PF = MAXN / 1024u;                /* 16-byte loads per lane per value */
+    __shared__ __attribute__((aligned(16))) uint16_t H[BUCKETS];
+    __shared__ uint16_t E[MAXN];
+    __shared__ __attribute__((aligned(16))) uint32_t Bw[MAXN / 4u + 4u];
+    __shared__ unsigned long long T[KS_WIN][TN];
     const uint32_t lane = threadIdx.x;
     const unsigned long long mine = 1ull << lane, below = mine - 1ull;
     uint32_t v = blockIdx.x;
     if (v >= bt.count) return;
-    for (uint32_t k = lane; k < KS_WIN * KS_TN; k += 64u) (&T[0][0])[k] = 0ull;
-    uint4 pf[4];
+    for (uint32_t k = lane; k < KS_WIN * TN; k += 64u) (&T[0][0])[k] = 0ull;
+    uint4 pf[PF];
     uint32_t pn = bt.in_len[v];
     {
         const uint8_t *s0 = bt.in + bt.in_off[v];
 #pragma unroll
-        for (uint32_t k = 0; k < 4u; k++) {
+        for (uint32_t k = 0; k < PF; k++) {
             const uint32_t at = 16u * (64u * k + lane);
             pf[k] = at < pn ? ln_ld16_safe(s0 + at, pn - at) : make_uint4(0, 0, 0, 0);
         }
@@ -408,19 +415,19 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
         const uint32_t n = pn;
         uint16_t *cand = sc.cand + (uint64_t)v * sc.cstride;
 #pragma unroll
-        for (uint32_t k = 0; k < 4u; k++) ((uint4 *)Bw)[64u * k + lane] = pf[k];
+        for (uint32_t k = 0; k < PF; k++) ((uint4 *)Bw)[64u * k + lane] = pf[k];
         const uint32_t vn = v + gridDim.x;
         if (vn < bt.count) {                       /* next value's bytes, in flight */
             pn = bt.in_len[vn];
             const uint8_t *s1 = bt.in + bt.in_off[vn];
 #pragma unroll
-            for (uint32_t k = 0; k < 4u; k++) {
+            for (uint32_t k = 0; k < PF; k++) {
                 const uint32_t at = 16u * (64u * k + lane);
                 pf[k] = at < pn ? ln_ld16_safe(s1 + at, pn - at) : make_uint4(0, 0, 0, 0);
             }
         }
         if (n >= 3u) {
-            for (uint32_t k = lane; k < KS_BUCKETS / 8u; k += 64u) ((uint4 *)H)[k] = make_uint4(0, 0, 0, 0);
+            for (uint32_t k = lane; k < BUCKETS / 8u; k += 64u) ((uint4 *)H)[k] = make_uint4(0, 0, 0, 0);
             ln_wave_fence();
             const uint32_t np = n - 2u;               /* positions 0 .. n-3 */
             for (uint32_t P = 0; P < np; P += 64u * KS_WIN) {
@@ -438,9 +445,9 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                     m[j] = ln_mix(ln_slot(tri[j]));
 #ifndef KS_ABL_T
                     if (act[j]) {
-                        __hip_atomic_fetch_or(&T[j][KS_T0 + ((m[j] >> 4) & 63u)], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_or(&T[j][KS_T1 + (m[j] >> 10)], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_or(&T[j][KS_T2 + (m[j] & 15u)], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_or(&T[j][T0 + ((m[j] >> IDB) & 63u)], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_or(&T[j][T1 + (m[j] >> (IDB + 6u))], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_or(&T[j][T2 + (m[j] & IDM)], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
 #endif
                 }
@@ -451,8 +458,8 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
 #ifdef KS_ABL_T
                     MB[j] = MS[j] = mine;
 #else
-                    MB[j] = T[j][KS_T0 + ((m[j] >> 4) & 63u)] & T[j][KS_T1 + (m[j] >> 10)];
-                    MS[j] = MB[j] & T[j][KS_T2 + (m[j] & 15u)];
+                    MB[j] = T[j][T0 + ((m[j] >> IDB) & 63u)] & T[j][T1 + (m[j] >> (IDB + 6u))];
+                    MS[j] = MB[j] & T[j][T2 + (m[j] & IDM)];
 #endif
                     if (!act[j]) MB[j] = MS[j] = 0ull;
                 }
@@ -461,9 +468,9 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                 for (uint32_t j = 0; j < KS_WIN; j++) {
 #ifndef KS_ABL_T
                     if (act[j]) {
-                        T[j][KS_T0 + ((m[j] >> 4) & 63u)] = 0ull;
-                        T[j][KS_T1 + (m[j] >> 10)] = 0ull;
-                        T[j][KS_T2 + (m[j] & 15u)] = 0ull;
+                        T[j][T0 + ((m[j] >> IDB) & 63u)] = 0ull;
+                        T[j][T1 + (m[j] >> (IDB + 6u))] = 0ull;
+                        T[j][T2 + (m[j] & IDM)] = 0ull;
                     }
 #endif
                 }
@@ -473,25 +480,25 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                 bool need = false;
 #pragma unroll
                 for (uint32_t j = 0; j < KS_WIN; j++) {
-                    const uint32_t bk = m[j] >> 4, id = m[j] & 15u;
-                    const uint32_t key = ((p[j] + 1u) << 4) | id;
+                    const uint32_t bk = m[j] >> IDB, id = m[j] & IDM;
+                    const uint32_t key = ((p[j] + 1u) << IDB) | id;
                     const unsigned long long ss = MS[j] & below, sb = MB[j] & ~MS[j] & below;
                     const uint32_t h = act[j] ? (uint32_t)H[bk] : 0u;
-                    const uint32_t eh = (act[j] && h) ? (uint32_t)E[(h >> 4) - 1u] : 0u;
+                    const uint32_t eh = (act[j] && h) ? (uint32_t)E[(h >> IDB) - 1u] : 0u;
                     /* skip link: latest earlier bucket position with another identity */
                     const uint32_t lsb = sb ? ks_hibit(sb) : lane;
                     const uint32_t ksb = (uint32_t)__shfl((int)key, (int)lsb);
-                    const uint32_t link = sb ? ksb : ((h & 15u) != id ? h : eh);
+                    const uint32_t link = sb ? ksb : ((h & IDM) != id ? h : eh);
                     if (act[j]) E[p[j]] = (uint16_t)link;
                     if (act[j] && (MB[j] >> lane) == 1ull) H[bk] = (uint16_t)key;
                     /* same-slot predecessor */
                     q1[j] = ss ? P + 64u * j + ks_hibit(ss) + 1u : 0u;    /* pos+1 */
                     cur[j] = (act[j] && !ss) ? h : 0u;
-                    if (cur[j] && (cur[j] & 15u) == id) { q1[j] = cur[j] >> 4; cur[j] = 0u; }
+                    if (cur[j] && (cur[j] & IDM) == id) { q1[j] = cur[j] >> IDB; cur[j] = 0u; }
                     /* the head's own link is eh, read above: the first hop is free */
                     if (cur[j]) {
                         cur[j] = eh;
-                        if (eh && (eh & 15u) == id) { q1[j] = eh >> 4; cur[j] = 0u; }
+                        if (eh && (eh & IDM) == id) { q1[j] = eh >> IDB; cur[j] = 0u; }
                     }
                     need |= cur[j] != 0u;
                 }
@@ -504,9 +511,9 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
 #pragma unroll
                     for (uint32_t j = 0; j < KS_WIN; j++) {
                         if (cur[j]) {
-                            const uint32_t e = E[(cur[j] >> 4) - 1u];
+                            const uint32_t e = E[(cur[j] >> IDB) - 1u];
                             cur[j] = e;
-                            if (e && (e & 15u) == (m[j] & 15u)) { q1[j] = e >> 4; cur[j] = 0u; }
+                            if (e && (e & IDM) == (m[j] & IDM)) { q1[j] = e >> IDB; cur[j] = 0u; }
                             need |= cur[j] != 0u;
                         }
                     }
@@ -1277,12 +1284,13 @@ size_t lzf_lane_scratch_per_value(uint32_t max_len)
     return (size_t)(lane_cstride(max_len) * 2u + lane_bstride(max_len) * 4u);
 }
 
-/* The default lane path takes the small class only: on longer values the
- * window generation is faster today; LZF_GPU_LANE_MID=1
- * routes values up to 64 KiB through the mid-class kernels as well. */
+/* The default lane path takes the small classes only (values <= 8 KiB): on
+ * longer values the window generation is faster today;
+ * LZF_GPU_LANE_MID=1 routes values up to 64 KiB through the mid-class
+ * kernels as well. */
 bool lzf_lane_compress_supported(uint32_t max_len)
 {
-    if (max_len <= KS_MAXN) return true;
+    if (max_len <= KS8_MAXN) return true;
     const char *e = getenv("LZF_GPU_LANE_MID");
     return max_len <= KM_MAXN && e && *e == '1';
 }
@@ -1317,13 +1325,15 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
     }
     /* the small-class kernel is persistent: as many one-wave workgroups as
      * stay resident (LDS-bound), each walking the batch */
+    const void *small_fn = b.max_len <= KS_MAXN ? (const void *)lzf_cand_small_kernel<4u, KS_MAXN>
+                                                : (const void *)lzf_cand_small_kernel<3u, KS8_MAXN>;
     uint32_t small_grid = 256u * 8u;
     {
         int dev = 0, cus = 0;
         hipFuncAttributes fa;
         if (hipGetDevice(&dev) == hipSuccess &&
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            hipFuncGetAttributes(&fa, (const void *)lzf_cand_small_kernel) == hipSuccess && cus > 0 &&
+            hipFuncGetAttributes(&fa, small_fn) == hipSuccess && cus > 0 &&
             fa.sharedSizeBytes > 0) {
             uint32_t per = (uint32_t)(160u * 1024u / fa.sharedSizeBytes);   /* LDS-bound residency */
             const char *pe_ = getenv("LZF_LANE_CAND_PER");            /* residency override */
@@ -1359,7 +1369,10 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
         if (pipe && i >= 2u && (e = hipStreamWaitEvent(s, ev[2 + h], 0)) != hipSuccess) return e;
         if (b.max_len <= KS_MAXN) {
             const uint32_t g = cnt < small_grid ? cnt : small_grid;
-            hipLaunchKernelGGL(lzf_cand_small_kernel, dim3(g), dim3(64), 0, s, c, sc[h]);
+            hipLaunchKernelGGL((lzf_cand_small_kernel<4u, KS_MAXN>), dim3(g), dim3(64), 0, s, c, sc[h]);
+        } else if (b.max_len <= KS8_MAXN) {
+            const uint32_t g = cnt < small_grid ? cnt : small_grid;
+            hipLaunchKernelGGL((lzf_cand_small_kernel<3u, KS8_MAXN>), dim3(g), dim3(64), 0, s, c, sc[h]);
         } else {
             hipLaunchKernelGGL(lzf_cand_mid_kernel, dim3(cnt), dim3(64), 0, s, c, sc[h]);
         }

@@ -92,7 +92,7 @@ def test_batch_compress_golden(golden, generation):
     assert not bad, f"{len(bad)} mismatches, first: {bad[:5]}"
 
 
-@pytest.mark.parametrize("nmax", [4096, 65536])
+@pytest.mark.parametrize("nmax", [4096, 8192, 65536])
 def test_batch_compress_golden_by_size(golden, generation, nmax):
     # batches whose largest value selects each kernel class of a generation
     # (a batch with any value past 64 KiB runs the window generation)
