@@ -71,7 +71,7 @@ int current_device_ok()
 
 /* Compress scratch of the lane generation (cand words + inserted bitmap),
  * one per (host thread, device), grown on demand up to LZF_GPU_SCRATCH_MB
- * (default 12 GiB; larger batches run in chunks).  A batch on another stream
+ * (default 24 GiB: 1 M values of 8 KiB in one chunk; larger batches run in chunks).  A batch on another stream
  * than the previous user waits for that user's kernels first. */
 struct Scratch {
     void *p = nullptr;
@@ -86,7 +86,7 @@ struct Scratch {
 size_t scratch_limit()
 {
     const char *e = getenv("LZF_GPU_SCRATCH_MB");
-    unsigned long long mb = e ? strtoull(e, nullptr, 10) : 12288ull;
+    unsigned long long mb = e ? strtoull(e, nullptr, 10) : 24576ull;
     if (mb < 1) mb = 1;
     return (size_t)mb << 20;
 }

@@ -281,6 +281,9 @@ hipError_t lzf_launch_decompress_lane(const LzfBatch &b, hipStream_t s)
 #ifndef KS_WIN
 #define KS_WIN      2u            /* small class: windows per step (2: 31.4 ms, 1: 33.1, 3: 36.9, 4: 36.3 on json4k) */
 #endif
+#ifndef KS8_WIN
+#define KS8_WIN     2u            /* 8 KiB small class: windows per step */
+#endif
 #define KS_MAXN     4096u         /* small class: 12-bit bucket, 4-bit identity, positions + 1 fit 12 bits */
 #define KS8_MAXN    8192u         /* small class, 8 KiB: 13-bit bucket, 3-bit identity, positions + 1 fit 13 bits */
 #define KM_BUCKETS  2048u         /* mid class */
@@ -382,7 +385,7 @@ __device__ __forceinline__ uint32_t ks_hibit(uint64_t m)
     return 63u - (uint32_t)__builtin_clzll(m);
 }
 
-template <uint32_t IDB, uint32_t MAXN>
+template <uint32_t IDB, uint32_t MAXN, uint32_t WIN>
 __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLaneScratch sc)
 {
     static_assert(MAXN <= LZF_WINDOW && ((MAXN - 1u) >> (16u - IDB)) == 0u, "entry [pos+1 | id] must fit 16 bits");
@@ -395,12 +398,12 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
     __shared__ __attribute__((aligned(16))) uint16_t H[BUCKETS];
     __shared__ uint16_t E[MAXN];
     __shared__ __attribute__((aligned(16))) uint32_t Bw[MAXN / 4u + 4u];
-    __shared__ unsigned long long T[KS_WIN][TN];
+    __shared__ unsigned long long T[WIN][TN];
     const uint32_t lane = threadIdx.x;
     const unsigned long long mine = 1ull << lane, below = mine - 1ull;
     uint32_t v = blockIdx.x;
     if (v >= bt.count) return;
-    for (uint32_t k = lane; k < KS_WIN * TN; k += 64u) (&T[0][0])[k] = 0ull;
+    for (uint32_t k = lane; k < WIN * TN; k += 64u) (&T[0][0])[k] = 0ull;
     uint4 pf[PF];
     uint32_t pn = bt.in_len[v];
     {
@@ -430,18 +433,18 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
             for (uint32_t k = lane; k < BUCKETS / 8u; k += 64u) ((uint4 *)H)[k] = make_uint4(0, 0, 0, 0);
             ln_wave_fence();
             const uint32_t np = n - 2u;               /* positions 0 .. n-3 */
-            for (uint32_t P = 0; P < np; P += 64u * KS_WIN) {
-                uint32_t p[KS_WIN], m[KS_WIN], tri[KS_WIN];
-                bool act[KS_WIN];
+            for (uint32_t P = 0; P < np; P += 64u * WIN) {
+                uint32_t p[WIN], m[WIN], tri[WIN];
+                bool act[WIN];
                 /* the step's byte reads first, in one LDS round trip */
 #pragma unroll
-                for (uint32_t j = 0; j < KS_WIN; j++) {
+                for (uint32_t j = 0; j < WIN; j++) {
                     p[j] = P + 64u * j + lane;
                     act[j] = p[j] < np;
                     tri[j] = ks_rd4(Bw, act[j] ? p[j] : 0u);
                 }
 #pragma unroll
-                for (uint32_t j = 0; j < KS_WIN; j++) {
+                for (uint32_t j = 0; j < WIN; j++) {
                     m[j] = ln_mix(ln_slot(tri[j]));
 #ifndef KS_ABL_T
                     if (act[j]) {
@@ -452,9 +455,9 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
 #endif
                 }
                 ln_wave_fence();
-                unsigned long long MB[KS_WIN], MS[KS_WIN];
+                unsigned long long MB[WIN], MS[WIN];
 #pragma unroll
-                for (uint32_t j = 0; j < KS_WIN; j++) {
+                for (uint32_t j = 0; j < WIN; j++) {
 #ifdef KS_ABL_T
                     MB[j] = MS[j] = mine;
 #else
@@ -465,7 +468,7 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                 }
                 ln_wave_fence();
 #pragma unroll
-                for (uint32_t j = 0; j < KS_WIN; j++) {
+                for (uint32_t j = 0; j < WIN; j++) {
 #ifndef KS_ABL_T
                     if (act[j]) {
                         T[j][T0 + ((m[j] >> IDB) & 63u)] = 0ull;
@@ -476,10 +479,10 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                 }
                 /* window j reads the heads after window j-1 wrote them (LDS
                  * ops of a wave execute in order) */
-                uint32_t q1[KS_WIN], cur[KS_WIN];
+                uint32_t q1[WIN], cur[WIN];
                 bool need = false;
 #pragma unroll
-                for (uint32_t j = 0; j < KS_WIN; j++) {
+                for (uint32_t j = 0; j < WIN; j++) {
                     const uint32_t bk = m[j] >> IDB, id = m[j] & IDM;
                     const uint32_t key = ((p[j] + 1u) << IDB) | id;
                     const unsigned long long ss = MS[j] & below, sb = MB[j] & ~MS[j] & below;
@@ -509,7 +512,7 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                 while (__ballot(need)) {
                     need = false;
 #pragma unroll
-                    for (uint32_t j = 0; j < KS_WIN; j++) {
+                    for (uint32_t j = 0; j < WIN; j++) {
                         if (cur[j]) {
                             const uint32_t e = E[(cur[j] >> IDB) - 1u];
                             cur[j] = e;
@@ -519,7 +522,7 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                     }
                 }
 #pragma unroll
-                for (uint32_t j = 0; j < KS_WIN; j++) {
+                for (uint32_t j = 0; j < WIN; j++) {
                     if (!act[j]) continue;
                     uint32_t w = 0u;
                     if (q1[j] > 1u) {                    /* q = q1 - 1 > 0 */
@@ -1325,8 +1328,8 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
     }
     /* the small-class kernel is persistent: as many one-wave workgroups as
      * stay resident (LDS-bound), each walking the batch */
-    const void *small_fn = b.max_len <= KS_MAXN ? (const void *)lzf_cand_small_kernel<4u, KS_MAXN>
-                                                : (const void *)lzf_cand_small_kernel<3u, KS8_MAXN>;
+    const void *small_fn = b.max_len <= KS_MAXN ? (const void *)lzf_cand_small_kernel<4u, KS_MAXN, KS_WIN>
+                                                : (const void *)lzf_cand_small_kernel<3u, KS8_MAXN, KS8_WIN>;
     uint32_t small_grid = 256u * 8u;
     {
         int dev = 0, cus = 0;
@@ -1369,10 +1372,10 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
         if (pipe && i >= 2u && (e = hipStreamWaitEvent(s, ev[2 + h], 0)) != hipSuccess) return e;
         if (b.max_len <= KS_MAXN) {
             const uint32_t g = cnt < small_grid ? cnt : small_grid;
-            hipLaunchKernelGGL((lzf_cand_small_kernel<4u, KS_MAXN>), dim3(g), dim3(64), 0, s, c, sc[h]);
+            hipLaunchKernelGGL((lzf_cand_small_kernel<4u, KS_MAXN, KS_WIN>), dim3(g), dim3(64), 0, s, c, sc[h]);
         } else if (b.max_len <= KS8_MAXN) {
             const uint32_t g = cnt < small_grid ? cnt : small_grid;
-            hipLaunchKernelGGL((lzf_cand_small_kernel<3u, KS8_MAXN>), dim3(g), dim3(64), 0, s, c, sc[h]);
+            hipLaunchKernelGGL((lzf_cand_small_kernel<3u, KS8_MAXN, KS8_WIN>), dim3(g), dim3(64), 0, s, c, sc[h]);
         } else {
             hipLaunchKernelGGL(lzf_cand_mid_kernel, dim3(cnt), dim3(64), 0, s, c, sc[h]);
         }
