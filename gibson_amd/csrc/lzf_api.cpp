@@ -137,11 +137,14 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s)
     return e;
 }
 
-/* smallest batch the lane generation takes (LZF_GPU_LANE_MIN overrides) */
-uint32_t lane_min_count()
+/* smallest batch the lane generation takes (LZF_GPU_LANE_MIN overrides):
+ * tools/crossover.py measured the crossover near 160 k values of 4 KiB and
+ * near 48 k values of 8 KiB (window64 is 2.2x slower per byte there) */
+uint32_t lane_min_count(uint32_t max_len)
 {
     const char *e = getenv("LZF_GPU_LANE_MIN");
-    return e ? (uint32_t)strtoul(e, nullptr, 10) : 163840u;
+    if (e) return (uint32_t)strtoul(e, nullptr, 10);
+    return max_len <= 4096u ? 163840u : 49152u;
 }
 
 hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
@@ -154,7 +157,7 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
          * generation: the lane parse runs one value per lane, so its time has a
          * floor of one whole value's parse (~5 ms); below ~160 k values one
          * wave per value finishes first (tools/crossover.py) */
-        return (lzf_lane_compress_supported(b.max_len) && b.count >= lane_min_count())
+        return (lzf_lane_compress_supported(b.max_len) && b.count >= lane_min_count(b.max_len))
                    ? lane_compress(b, s)
                    : lzf_launch_compress(b, s);
     }
@@ -617,7 +620,8 @@ const char *lzf_gpu_kernel_info(void)
         break;
     default:
         s = std::string("compress=lane(cand+parse; window64 past 8 KiB or below ") +
-            std::to_string(lane_min_count()) + " values) decompress=" +
+            std::to_string(lane_min_count(4096u)) + " values of <= 4 KiB / " +
+            std::to_string(lane_min_count(8192u)) + " of <= 8 KiB) decompress=" +
             (lane_decoder() ? "lane" : lzf_decompress_kernel_name());
         break;
     }

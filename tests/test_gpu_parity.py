@@ -298,7 +298,7 @@ CONFIGS = [
     # (kind, seed, n, count) -- scaled batches of configs 2..5
     (1, 0x5EED0002, 4096, 65536),
     (2, 0x5EED0003, 65536, 2048),
-    (0, 0x5EED0004, 8192, 16384),
+    (0, 0x5EED0004, 8192, 65536),   # >= 49152 values: the 8 KiB lane class
     (3, 0x5EED0005, 16384, 8192),
 ]
 

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Compress time by batch size for the lane and window generations (json4k
-values): where does the lane generation start to pay?  The lane parse runs
+"""Compress time by batch size for the lane and window generations: where
+does the lane generation start to pay?  usage: crossover.py [KIND N]
+(default json4k: 1 4096).  The lane parse runs
 one value per lane, so a small batch leaves the GPU mostly idle while each
 lane walks its whole value."""
 import os
@@ -12,11 +13,13 @@ import torch  # noqa: E402
 
 import gibson_amd  # noqa: E402
 
-n = 4096
+kind = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 N = 1 << 20
+os.environ["LZF_GPU_LANE_MIN"] = "0"
 dev = torch.device("cuda")
 src = torch.empty(N * n, dtype=torch.uint8, device=dev)
-gibson_amd.synth_fill(1, 0x5EED0002, 0, 1, N, n, src)
+gibson_amd.synth_fill(kind, 0x5EED0002, 0, 1, N, n, src)
 off = torch.arange(N, dtype=torch.int64, device=dev) * n
 ln = torch.full((N,), n, dtype=torch.int32, device=dev)
 cap = torch.full((N,), n - 4, dtype=torch.int32, device=dev)
