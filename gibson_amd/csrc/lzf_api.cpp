@@ -153,7 +153,7 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
     case GEN_SERIAL: return lzf_launch_compress_serial(b, s);
     case GEN_WINDOW: return lzf_launch_compress(b, s);
     default:
-        /* batches with values past 8 KiB, and small batches, go to the window
+        /* batches with values past 8 KiB (16 KiB with LZF_GPU_LANE_RING=1), and small batches, go to the window
          * generation: the lane parse runs one value per lane, so its time has a
          * floor of one whole value's parse (~5 ms); below ~160 k values one
          * wave per value finishes first (tools/crossover.py) */

@@ -546,6 +546,180 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
     }
 }
 
+/* Small class, 16 KiB ("ring" form: values <= 16 KiB, so positions reach
+ * 8 KiB past the window).  The value's bytes are staged whole as above; the
+ * bucket heads are u32 [pos+1 | identity:4] (4096 buckets, 16 KiB) and the
+ * skip links are kept only for the last 8192 positions, in a ring of u32
+ * (32 KiB), which is all a candidate inside the window can reach.  A head or
+ * link whose position is more than 8192 before p is outside p's window
+ * (src/lzf_c.c:153 off < MAX_OFF) and ends the lookup: so is every older one.
+ * The links of the step in flight go to S first and join the ring after the
+ * step's walks, so that a walk never reads a ring slot the step overwrote.
+ * LDS 66.8 KiB: 2 values per CU.
+ *
+ * Opt-in (LZF_GPU_LANE_RING=1): against window64 at 256 K-1 M values of
+ * 16 KiB it is 1.8x faster on Zipf text and 1.24x on sentence text, but
+ * 0.92x on the mixed-entropy values of BASELINE configs[4] (its random
+ * segments make every bucket walk, at 2 values per CU). */
+#define KR_MAXN 16384u
+#ifndef KR_WIN
+#define KR_WIN  2u
+#endif
+template <uint32_t WIN>
+__global__ __launch_bounds__(64) void lzf_cand_ring_kernel(LzfBatch bt, LzfLaneScratch sc)
+{
+    constexpr uint32_t IDB = 4u, IDM = 15u, BUCKETS = 4096u, RING = LZF_WINDOW;
+    constexpr uint32_t T0 = 0u, T1 = 64u, T2 = 128u, TN = 144u;   /* digits as at 4 KiB */
+    constexpr uint32_t PF = KR_MAXN / 1024u;
+    __shared__ __attribute__((aligned(16))) uint32_t H[BUCKETS];
+    __shared__ uint32_t E[RING];
+    __shared__ uint32_t S[64u * WIN];
+    __shared__ __attribute__((aligned(16))) uint32_t Bw[KR_MAXN / 4u + 4u];
+    __shared__ unsigned long long T[WIN][TN];
+    const uint32_t lane = threadIdx.x;
+    const unsigned long long mine = 1ull << lane, below = mine - 1ull;
+    uint32_t v = blockIdx.x;
+    if (v >= bt.count) return;
+    for (uint32_t k = lane; k < WIN * TN; k += 64u) (&T[0][0])[k] = 0ull;
+    uint4 pf[PF];
+    uint32_t pn = bt.in_len[v];
+    {
+        const uint8_t *s0 = bt.in + bt.in_off[v];
+#pragma unroll
+        for (uint32_t k = 0; k < PF; k++) {
+            const uint32_t at = 16u * (64u * k + lane);
+            pf[k] = at < pn ? ln_ld16_safe(s0 + at, pn - at) : make_uint4(0, 0, 0, 0);
+        }
+    }
+    while (v < bt.count) {
+        const uint32_t n = pn;
+        uint16_t *cand = sc.cand + (uint64_t)v * sc.cstride;
+#pragma unroll
+        for (uint32_t k = 0; k < PF; k++) ((uint4 *)Bw)[64u * k + lane] = pf[k];
+        const uint32_t vn = v + gridDim.x;
+        if (vn < bt.count) {                       /* next value's bytes, in flight */
+            pn = bt.in_len[vn];
+            const uint8_t *s1 = bt.in + bt.in_off[vn];
+#pragma unroll
+            for (uint32_t k = 0; k < PF; k++) {
+                const uint32_t at = 16u * (64u * k + lane);
+                pf[k] = at < pn ? ln_ld16_safe(s1 + at, pn - at) : make_uint4(0, 0, 0, 0);
+            }
+        }
+        if (n >= 3u) {
+            for (uint32_t k = lane; k < BUCKETS / 4u; k += 64u) ((uint4 *)H)[k] = make_uint4(0, 0, 0, 0);
+            ln_wave_fence();
+            const uint32_t np = n - 2u;               /* positions 0 .. n-3 */
+            for (uint32_t P = 0; P < np; P += 64u * WIN) {
+                uint32_t p[WIN], m[WIN], tri[WIN];
+                bool act[WIN];
+#pragma unroll
+                for (uint32_t j = 0; j < WIN; j++) {
+                    p[j] = P + 64u * j + lane;
+                    act[j] = p[j] < np;
+                    tri[j] = ks_rd4(Bw, act[j] ? p[j] : 0u);
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < WIN; j++) {
+                    m[j] = ln_mix(ln_slot(tri[j]));
+                    if (act[j]) {
+                        __hip_atomic_fetch_or(&T[j][T0 + ((m[j] >> IDB) & 63u)], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_or(&T[j][T1 + (m[j] >> (IDB + 6u))], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_or(&T[j][T2 + (m[j] & IDM)], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                ln_wave_fence();
+                unsigned long long MB[WIN], MS[WIN];
+#pragma unroll
+                for (uint32_t j = 0; j < WIN; j++) {
+                    MB[j] = T[j][T0 + ((m[j] >> IDB) & 63u)] & T[j][T1 + (m[j] >> (IDB + 6u))];
+                    MS[j] = MB[j] & T[j][T2 + (m[j] & IDM)];
+                    if (!act[j]) MB[j] = MS[j] = 0ull;
+                }
+                ln_wave_fence();
+#pragma unroll
+                for (uint32_t j = 0; j < WIN; j++) {
+                    if (act[j]) {
+                        T[j][T0 + ((m[j] >> IDB) & 63u)] = 0ull;
+                        T[j][T1 + (m[j] >> (IDB + 6u))] = 0ull;
+                        T[j][T2 + (m[j] & IDM)] = 0ull;
+                    }
+                }
+                /* an entry x = [y+1 | id] is inside p's window iff y + 8192 >= p;
+                 * the link of position y is in S while y belongs to this step */
+#define KR_INW(x_, p_) ((x_) != 0u && ((x_) >> IDB) + (RING - 1u) >= (p_))
+#define KR_LINK(y_) ((y_) >= P ? S[(y_) - P] : E[(y_) & (RING - 1u)])
+                uint32_t q1[WIN], cur[WIN];
+                bool need = false;
+#pragma unroll
+                for (uint32_t j = 0; j < WIN; j++) {
+                    const uint32_t bk = m[j] >> IDB, id = m[j] & IDM;
+                    const uint32_t key = ((p[j] + 1u) << IDB) | id;
+                    const unsigned long long ss = MS[j] & below, sb = MB[j] & ~MS[j] & below;
+                    const uint32_t h0 = act[j] ? H[bk] : 0u;
+                    const uint32_t h = KR_INW(h0, p[j]) ? h0 : 0u;
+                    uint32_t eh = h ? KR_LINK((h >> IDB) - 1u) : 0u;
+                    if (!KR_INW(eh, p[j])) eh = 0u;
+                    /* skip link: latest earlier bucket position with another identity */
+                    const uint32_t lsb = sb ? ks_hibit(sb) : lane;
+                    const uint32_t ksb = (uint32_t)__shfl((int)key, (int)lsb);
+                    const uint32_t link = sb ? ksb : ((h & IDM) != id ? h : eh);
+                    if (act[j]) S[p[j] - P] = link;
+                    if (act[j] && (MB[j] >> lane) == 1ull) H[bk] = key;
+                    /* same-slot predecessor (pos+1), inside the window */
+                    q1[j] = ss ? P + 64u * j + ks_hibit(ss) + 1u : 0u;
+                    cur[j] = (act[j] && !ss) ? h : 0u;
+                    if (cur[j] && (cur[j] & IDM) == id) { q1[j] = cur[j] >> IDB; cur[j] = 0u; }
+                    if (cur[j]) {
+                        cur[j] = eh;
+                        if (eh && (eh & IDM) == id) { q1[j] = eh >> IDB; cur[j] = 0u; }
+                    }
+                    need |= cur[j] != 0u;
+                }
+                ln_wave_fence();
+                while (__ballot(need)) {
+                    need = false;
+#pragma unroll
+                    for (uint32_t j = 0; j < WIN; j++) {
+                        if (cur[j]) {
+                            uint32_t e = KR_LINK((cur[j] >> IDB) - 1u);
+                            if (!KR_INW(e, p[j])) e = 0u;
+                            cur[j] = e;
+                            if (e && (e & IDM) == (m[j] & IDM)) { q1[j] = e >> IDB; cur[j] = 0u; }
+                            need |= cur[j] != 0u;
+                        }
+                    }
+                }
+#undef KR_INW
+#undef KR_LINK
+#pragma unroll
+                for (uint32_t j = 0; j < WIN; j++) {
+                    if (!act[j]) continue;
+                    uint32_t w = 0u;
+                    if (q1[j] > 1u) {                    /* q = q1 - 1 > 0, p - q - 1 < 8192 */
+                        const uint32_t q = q1[j] - 1u;
+                        const uint32_t x0 = tri[j] ^ ks_rd4(Bw, q);
+                        const uint32_t x1 = ks_rd4(Bw, p[j] + 4u) ^ ks_rd4(Bw, q + 4u);
+                        const uint64_t xx = ((uint64_t)x1 << 32) | x0;
+                        uint32_t k = xx ? (uint32_t)__builtin_ctzll(xx) >> 3 : 8u;
+                        const uint32_t avail = n - p[j];
+                        if (k > avail) k = avail;
+                        w = (k1_code(k) << 13) | (p[j] - q - 1u);
+                    }
+                    cand[p[j]] = (uint16_t)w;
+                }
+                /* the step's links join the ring (every walk of the step is done) */
+#pragma unroll
+                for (uint32_t j = 0; j < WIN; j++)
+                    if (act[j]) E[p[j] & (RING - 1u)] = S[64u * j + lane];
+                ln_wave_fence();
+            }
+        }
+        ln_wave_fence();
+        v = vn;
+    }
+}
+
 /* Mid class (values <= 64 KiB).  LDS: bucket heads [pos+1:16 | mix:16]
  * (8 KiB), a ring of the head each position displaced (its bucket
  * predecessor's key) over the last 8192 positions (32 KiB), and the keys of
@@ -1287,13 +1461,21 @@ size_t lzf_lane_scratch_per_value(uint32_t max_len)
     return (size_t)(lane_cstride(max_len) * 2u + lane_bstride(max_len) * 4u);
 }
 
-/* The default lane path takes the small classes only (values <= 8 KiB): on
- * longer values the window generation is faster today;
+/* The default lane path takes the small classes only (values <= 8 KiB, and
+ * <= 16 KiB with LZF_GPU_LANE_RING=1): on longer values the window
+ * generation is faster today;
  * LZF_GPU_LANE_MID=1 routes values up to 64 KiB through the mid-class
  * kernels as well. */
+static bool lane_ring_enabled()
+{
+    const char *r = getenv("LZF_GPU_LANE_RING");
+    return r && *r == '1';
+}
+
 bool lzf_lane_compress_supported(uint32_t max_len)
 {
     if (max_len <= KS8_MAXN) return true;
+    if (max_len <= KR_MAXN && lane_ring_enabled()) return true;
     const char *e = getenv("LZF_GPU_LANE_MID");
     return max_len <= KM_MAXN && e && *e == '1';
 }
@@ -1328,8 +1510,10 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
     }
     /* the small-class kernel is persistent: as many one-wave workgroups as
      * stay resident (LDS-bound), each walking the batch */
-    const void *small_fn = b.max_len <= KS_MAXN ? (const void *)lzf_cand_small_kernel<4u, KS_MAXN, KS_WIN>
-                                                : (const void *)lzf_cand_small_kernel<3u, KS8_MAXN, KS8_WIN>;
+    const void *small_fn = b.max_len <= KS_MAXN    ? (const void *)lzf_cand_small_kernel<4u, KS_MAXN, KS_WIN>
+                           : b.max_len <= KS8_MAXN ? (const void *)lzf_cand_small_kernel<3u, KS8_MAXN, KS8_WIN>
+                                                   : (const void *)lzf_cand_ring_kernel<KR_WIN>;
+    const bool ring = b.max_len > KS8_MAXN && b.max_len <= KR_MAXN && lane_ring_enabled();
     uint32_t small_grid = 256u * 8u;
     {
         int dev = 0, cus = 0;
@@ -1376,6 +1560,9 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
         } else if (b.max_len <= KS8_MAXN) {
             const uint32_t g = cnt < small_grid ? cnt : small_grid;
             hipLaunchKernelGGL((lzf_cand_small_kernel<3u, KS8_MAXN, KS8_WIN>), dim3(g), dim3(64), 0, s, c, sc[h]);
+        } else if (ring) {
+            const uint32_t g = cnt < small_grid ? cnt : small_grid;
+            hipLaunchKernelGGL((lzf_cand_ring_kernel<KR_WIN>), dim3(g), dim3(64), 0, s, c, sc[h]);
         } else {
             hipLaunchKernelGGL(lzf_cand_mid_kernel, dim3(cnt), dim3(64), 0, s, c, sc[h]);
         }

@@ -92,7 +92,7 @@ def test_batch_compress_golden(golden, generation):
     assert not bad, f"{len(bad)} mismatches, first: {bad[:5]}"
 
 
-@pytest.mark.parametrize("nmax", [4096, 8192, 65536])
+@pytest.mark.parametrize("nmax", [4096, 8192, 16384, 65536])
 def test_batch_compress_golden_by_size(golden, generation, nmax):
     # batches whose largest value selects each kernel class of a generation
     # (a batch with any value past 64 KiB runs the window generation)
@@ -176,6 +176,30 @@ def test_lane_mid_class(oracle, monkeypatch):
 
 
 @pytest.mark.parametrize("align", [16, 3])
+def test_lane_ring_class(oracle, monkeypatch, align):
+    # the 16 KiB ring form of the cand kernel (values 8-16 KiB, opt-in): links
+    # kept for the last 8 KiB of positions, window tests on heads and links
+    from tests.gpu_batch import gpu_compress, gpu_decompress
+    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.setenv("LZF_GPU_LANE_RING", "1")
+    rnd = random.Random(33 + align)
+    vals = []
+    for i in range(1500):
+        n = rnd.choice([rnd.randint(1, 700), rnd.randint(8000, 16384), 16384])
+        v = synth(rnd.randrange(6), 0x5EED00F8, i, n)
+        if rnd.random() < 0.1:
+            v = bytes(rnd.choice(b"abc") for _ in range(n))
+        vals.append(v)
+    caps = [rnd.choice([max(1, len(v) - 4), len(v) + len(v) // 16 + 64, rnd.randint(1, len(v) + 64)])
+            for v in vals]
+    exp = [oracle.compress(v, c) for v, c in zip(vals, caps)]
+    assert gpu_compress(vals, caps, align=align) == exp
+    streams = [r for r in exp if r]
+    origs = [v for v, r in zip(vals, exp) if r]
+    assert gpu_decompress(streams, [len(v) for v in origs]) == [(v, 0) for v in origs]
+
+
+@pytest.mark.parametrize("align", [16, 3])
 def test_wave_parse(oracle, monkeypatch, align):
     # the wave form of the parse kernel (64 positions per step, opt-in):
     # every size class edge of a window, caps that run out inside a window
@@ -216,11 +240,14 @@ def test_lane_order_repair_path(oracle, monkeypatch):
         assert gpu_compress(vals, caps) == [oracle.compress(v, c) for v, c in zip(vals, caps)]
 
 
-@pytest.mark.parametrize("nmax", [4096, 8192, 9000])
-def test_random_differential(oracle, generation, nmax):
+@pytest.mark.parametrize("nmax", [4096, 8192, 9000, 16384])
+def test_random_differential(oracle, generation, nmax, monkeypatch):
     # nmax 8192: the batch fits the non-wrapping ring/chain kernel; 9000:
-    # the wrapping one (the kernel is chosen per batch from max_len)
+    # the wrapping one (the kernel is chosen per batch from max_len); 16384
+    # takes the lane generation's ring class (opt-in)
     from tests.gpu_batch import gpu_compress, gpu_decompress
+    if nmax == 16384:
+        monkeypatch.setenv("LZF_GPU_LANE_RING", "1")
     rnd = random.Random(7 + nmax)
     vals, caps = [], []
     for it in range(3000):
@@ -299,13 +326,18 @@ CONFIGS = [
     (1, 0x5EED0002, 4096, 65536),
     (2, 0x5EED0003, 65536, 2048),
     (0, 0x5EED0004, 8192, 65536),   # >= 49152 values: the 8 KiB lane class
-    (3, 0x5EED0005, 16384, 8192),
+    (3, 0x5EED0005, 16384, 65536),  # >= 49152 values: the ring lane class when asked for
 ]
 
 
+@pytest.mark.parametrize("ring", [False, True])
 @pytest.mark.parametrize("kind,seed,n,count", CONFIGS)
-def test_full_size_roundtrip(kind, seed, n, count, oracle):
+def test_full_size_roundtrip(kind, seed, n, count, oracle, ring, monkeypatch):
     import gibson_amd
+    if ring:
+        if n != 16384:
+            pytest.skip("the ring class covers values of 8-16 KiB")
+        monkeypatch.setenv("LZF_GPU_LANE_RING", "1")
     dev = "cuda"
     src = torch.empty(count * n, dtype=torch.uint8, device=dev)
     gibson_amd.synth_fill(kind, seed, 0, 1, count, n, src)
