@@ -138,13 +138,15 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s)
 }
 
 /* smallest batch the lane generation takes (LZF_GPU_LANE_MIN overrides):
- * tools/crossover.py measured the crossover near 160 k values of 4 KiB and
- * near 48 k values of 8 KiB (window64 is 2.2x slower per byte there) */
+ * tools/crossover.py measured the crossover near 160 k values of 4 KiB,
+ * near 48 k values of 8 KiB (window64 is 2.2x slower per byte there) and
+ * near 160 k values of 16 KiB (mixed entropy: 86.0 vs 82.0 ms at 128 K,
+ * 136.8 vs 163.8 ms at 256 K) */
 uint32_t lane_min_count(uint32_t max_len)
 {
     const char *e = getenv("LZF_GPU_LANE_MIN");
     if (e) return (uint32_t)strtoul(e, nullptr, 10);
-    return max_len <= 4096u ? 163840u : 49152u;
+    return (max_len > 4096u && max_len <= 8192u) ? 49152u : 163840u;
 }
 
 hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
@@ -153,7 +155,7 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
     case GEN_SERIAL: return lzf_launch_compress_serial(b, s);
     case GEN_WINDOW: return lzf_launch_compress(b, s);
     default:
-        /* batches with values past 8 KiB (16 KiB with LZF_GPU_LANE_RING=1), and small batches, go to the window
+        /* batches with values past 16 KiB, and small batches, go to the window
          * generation: the lane parse runs one value per lane, so its time has a
          * floor of one whole value's parse (~5 ms); below ~160 k values one
          * wave per value finishes first (tools/crossover.py) */
@@ -619,9 +621,10 @@ const char *lzf_gpu_kernel_info(void)
             lzf_decompress_kernel_name();
         break;
     default:
-        s = std::string("compress=lane(cand+parse; window64 past 8 KiB or below ") +
+        s = std::string("compress=lane(cand+parse; window64 past 16 KiB or below ") +
             std::to_string(lane_min_count(4096u)) + " values of <= 4 KiB / " +
-            std::to_string(lane_min_count(8192u)) + " of <= 8 KiB) decompress=" +
+            std::to_string(lane_min_count(8192u)) + " of <= 8 KiB / " +
+            std::to_string(lane_min_count(16384u)) + " of <= 16 KiB) decompress=" +
             (lane_decoder() ? "lane" : lzf_decompress_kernel_name());
         break;
     }

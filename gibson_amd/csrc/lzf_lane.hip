@@ -549,18 +549,22 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
 /* Small class, 16 KiB ("ring" form: values <= 16 KiB, so positions reach
  * 8 KiB past the window).  The value's bytes are staged whole as above; the
  * bucket heads are u32 [pos+1 | identity:4] (4096 buckets, 16 KiB) and the
- * skip links are kept only for the last 8192 positions, in a ring of u32
- * (32 KiB), which is all a candidate inside the window can reach.  A head or
+ * skip links are kept only for the last 8192 positions, which is all a
+ * candidate inside the window can reach, in a ring of u16 (16 KiB): a link
+ * is [d:13 | identity bits 0-2], d = distance back to the target (0: none;
+ * a target 8192 or more back is outside every later window).  A target whose
+ * three stored identity bits match is confirmed from its bytes (its full slot
+ * mix, read in the same LDS round trip as its own link).  A head or
  * link whose position is more than 8192 before p is outside p's window
  * (src/lzf_c.c:153 off < MAX_OFF) and ends the lookup: so is every older one.
  * The links of the step in flight go to S first and join the ring after the
  * step's walks, so that a walk never reads a ring slot the step overwrote.
- * LDS 66.8 KiB: 2 values per CU.
+ * LDS 50.6 KiB: 3 values per CU (u32 links: 66.8 KiB, 2 per CU).
  *
- * Opt-in (LZF_GPU_LANE_RING=1): against window64 at 256 K-1 M values of
- * 16 KiB it is 1.8x faster on Zipf text and 1.24x on sentence text, but
- * 0.92x on the mixed-entropy values of BASELINE configs[4] (its random
- * segments make every bucket walk, at 2 values per CU). */
+ * Against window64 at 1 M values of 16 KiB (tools/crossover.py): mixed
+ * entropy (BASELINE configs[4]) 570 vs 648 ms, Zipf text 437 vs 938 ms,
+ * sentence text 473 vs 676 ms.  With u32 links (2 values per CU) it was
+ * 702 / 523 / 549 ms. */
 #define KR_MAXN 16384u
 #ifndef KR_WIN
 #define KR_WIN  2u
@@ -572,8 +576,8 @@ __global__ __launch_bounds__(64) void lzf_cand_ring_kernel(LzfBatch bt, LzfLaneS
     constexpr uint32_t T0 = 0u, T1 = 64u, T2 = 128u, TN = 144u;   /* digits as at 4 KiB */
     constexpr uint32_t PF = KR_MAXN / 1024u;
     __shared__ __attribute__((aligned(16))) uint32_t H[BUCKETS];
-    __shared__ uint32_t E[RING];
-    __shared__ uint32_t S[64u * WIN];
+    __shared__ uint16_t E[RING];
+    __shared__ uint16_t S[64u * WIN];
     __shared__ __attribute__((aligned(16))) uint32_t Bw[KR_MAXN / 4u + 4u];
     __shared__ unsigned long long T[WIN][TN];
     const uint32_t lane = threadIdx.x;
@@ -645,11 +649,11 @@ __global__ __launch_bounds__(64) void lzf_cand_ring_kernel(LzfBatch bt, LzfLaneS
                         T[j][T2 + (m[j] & IDM)] = 0ull;
                     }
                 }
-                /* an entry x = [y+1 | id] is inside p's window iff y + 8192 >= p;
+                /* a head x = [y+1 | id] is inside p's window iff y + 8192 >= p;
                  * the link of position y is in S while y belongs to this step */
 #define KR_INW(x_, p_) ((x_) != 0u && ((x_) >> IDB) + (RING - 1u) >= (p_))
-#define KR_LINK(y_) ((y_) >= P ? S[(y_) - P] : E[(y_) & (RING - 1u)])
-                uint32_t q1[WIN], cur[WIN];
+#define KR_LINK(y_) ((uint32_t)((y_) >= P ? S[(y_) - P] : E[(y_) & (RING - 1u)]))
+                uint32_t q1[WIN], cp[WIN], ci[WIN];   /* candidate: pos+1 (0: none), id bits 0-2 */
                 bool need = false;
 #pragma unroll
                 for (uint32_t j = 0; j < WIN; j++) {
@@ -658,35 +662,55 @@ __global__ __launch_bounds__(64) void lzf_cand_ring_kernel(LzfBatch bt, LzfLaneS
                     const unsigned long long ss = MS[j] & below, sb = MB[j] & ~MS[j] & below;
                     const uint32_t h0 = act[j] ? H[bk] : 0u;
                     const uint32_t h = KR_INW(h0, p[j]) ? h0 : 0u;
-                    uint32_t eh = h ? KR_LINK((h >> IDB) - 1u) : 0u;
-                    if (!KR_INW(eh, p[j])) eh = 0u;
+                    /* the head's link: target pos+1 (0: none or out of window), id bits */
+                    uint32_t ey = 0u, ei = 0u;
+                    if (h) {
+                        const uint32_t e = KR_LINK((h >> IDB) - 1u);
+                        ey = e ? (h >> IDB) - (e >> 3) : 0u;
+                        if (ey + (RING - 1u) < p[j]) ey = 0u;
+                        ei = e & 7u;
+                    }
                     /* skip link: latest earlier bucket position with another identity */
                     const uint32_t lsb = sb ? ks_hibit(sb) : lane;
                     const uint32_t ksb = (uint32_t)__shfl((int)key, (int)lsb);
-                    const uint32_t link = sb ? ksb : ((h & IDM) != id ? h : eh);
-                    if (act[j]) S[p[j] - P] = link;
+                    uint32_t ty, ti;                                  /* link target pos+1, id bits */
+                    if (sb) { ty = ksb >> IDB; ti = ksb & 7u; }
+                    else if (h && (h & IDM) != id) { ty = h >> IDB; ti = h & 7u; }
+                    else { ty = ey; ti = ei; }
+                    const uint32_t d = p[j] + 1u - ty;                /* >= 1 when ty != 0 */
+                    if (act[j]) S[p[j] - P] = (uint16_t)((ty && d < RING) ? ((d << 3) | ti) : 0u);
                     if (act[j] && (MB[j] >> lane) == 1ull) H[bk] = key;
                     /* same-slot predecessor (pos+1), inside the window */
                     q1[j] = ss ? P + 64u * j + ks_hibit(ss) + 1u : 0u;
-                    cur[j] = (act[j] && !ss) ? h : 0u;
-                    if (cur[j] && (cur[j] & IDM) == id) { q1[j] = cur[j] >> IDB; cur[j] = 0u; }
-                    if (cur[j]) {
-                        cur[j] = eh;
-                        if (eh && (eh & IDM) == id) { q1[j] = eh >> IDB; cur[j] = 0u; }
+                    cp[j] = 0u;
+                    ci[j] = ei;
+                    if (act[j] && !ss && h) {
+                        if ((h & IDM) == id) q1[j] = h >> IDB;
+                        else cp[j] = ey;                              /* walk from the head's link */
                     }
-                    need |= cur[j] != 0u;
+                    need |= cp[j] != 0u;
                 }
                 ln_wave_fence();
+                /* per hop: the candidate's link and bytes in one LDS round trip;
+                 * it is the same-slot predecessor iff its slot mix equals mine */
                 while (__ballot(need)) {
                     need = false;
 #pragma unroll
                     for (uint32_t j = 0; j < WIN; j++) {
-                        if (cur[j]) {
-                            uint32_t e = KR_LINK((cur[j] >> IDB) - 1u);
-                            if (!KR_INW(e, p[j])) e = 0u;
-                            cur[j] = e;
-                            if (e && (e & IDM) == (m[j] & IDM)) { q1[j] = e >> IDB; cur[j] = 0u; }
-                            need |= cur[j] != 0u;
+                        if (cp[j]) {
+                            const uint32_t y = cp[j] - 1u;
+                            const uint32_t e = KR_LINK(y);
+                            const uint32_t ty = ks_rd4(Bw, y);
+                            if (ci[j] == (m[j] & 7u) && ln_mix(ln_slot(ty)) == m[j]) {
+                                q1[j] = cp[j];
+                                cp[j] = 0u;
+                            } else {
+                                uint32_t ny = e ? cp[j] - (e >> 3) : 0u;
+                                if (ny + (RING - 1u) < p[j]) ny = 0u;
+                                cp[j] = ny;
+                                ci[j] = e & 7u;
+                                need |= ny != 0u;
+                            }
                         }
                     }
                 }
@@ -1461,15 +1485,15 @@ size_t lzf_lane_scratch_per_value(uint32_t max_len)
     return (size_t)(lane_cstride(max_len) * 2u + lane_bstride(max_len) * 4u);
 }
 
-/* The default lane path takes the small classes only (values <= 8 KiB, and
- * <= 16 KiB with LZF_GPU_LANE_RING=1): on longer values the window
+/* The default lane path takes the small classes only (values <= 16 KiB;
+ * LZF_GPU_LANE_RING=0 stops it at 8 KiB): on longer values the window
  * generation is faster today;
  * LZF_GPU_LANE_MID=1 routes values up to 64 KiB through the mid-class
  * kernels as well. */
 static bool lane_ring_enabled()
 {
-    const char *r = getenv("LZF_GPU_LANE_RING");
-    return r && *r == '1';
+    const char *r = getenv("LZF_GPU_LANE_RING");     /* "0" turns the ring class off */
+    return !(r && *r == '0');
 }
 
 bool lzf_lane_compress_supported(uint32_t max_len)

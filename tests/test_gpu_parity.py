@@ -177,7 +177,7 @@ def test_lane_mid_class(oracle, monkeypatch):
 
 @pytest.mark.parametrize("align", [16, 3])
 def test_lane_ring_class(oracle, monkeypatch, align):
-    # the 16 KiB ring form of the cand kernel (values 8-16 KiB, opt-in): links
+    # the 16 KiB ring form of the cand kernel (values 8-16 KiB): links
     # kept for the last 8 KiB of positions, window tests on heads and links
     from tests.gpu_batch import gpu_compress, gpu_decompress
     monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
@@ -244,7 +244,7 @@ def test_lane_order_repair_path(oracle, monkeypatch):
 def test_random_differential(oracle, generation, nmax, monkeypatch):
     # nmax 8192: the batch fits the non-wrapping ring/chain kernel; 9000:
     # the wrapping one (the kernel is chosen per batch from max_len); 16384
-    # takes the lane generation's ring class (opt-in)
+    # takes the lane generation's ring class
     from tests.gpu_batch import gpu_compress, gpu_decompress
     if nmax == 16384:
         monkeypatch.setenv("LZF_GPU_LANE_RING", "1")
@@ -326,7 +326,7 @@ CONFIGS = [
     (1, 0x5EED0002, 4096, 65536),
     (2, 0x5EED0003, 65536, 2048),
     (0, 0x5EED0004, 8192, 65536),   # >= 49152 values: the 8 KiB lane class
-    (3, 0x5EED0005, 16384, 65536),  # >= 49152 values: the ring lane class when asked for
+    (3, 0x5EED0005, 16384, 65536),  # the ring lane class, and window64
 ]
 
 
@@ -334,10 +334,11 @@ CONFIGS = [
 @pytest.mark.parametrize("kind,seed,n,count", CONFIGS)
 def test_full_size_roundtrip(kind, seed, n, count, oracle, ring, monkeypatch):
     import gibson_amd
-    if ring:
-        if n != 16384:
-            pytest.skip("the ring class covers values of 8-16 KiB")
-        monkeypatch.setenv("LZF_GPU_LANE_RING", "1")
+    if n == 16384:
+        # the ring lane class (default) and, without it, window64
+        monkeypatch.setenv("LZF_GPU_LANE_RING", "1" if ring else "0")
+    elif ring:
+        pytest.skip("the ring class covers values of 8-16 KiB")
     dev = "cuda"
     src = torch.empty(count * n, dtype=torch.uint8, device=dev)
     gibson_amd.synth_fill(kind, seed, 0, 1, count, n, src)
