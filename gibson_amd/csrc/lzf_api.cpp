@@ -71,7 +71,7 @@ int current_device_ok()
 
 /* Compress scratch of the lane generation (cand words + inserted bitmap),
  * one per (host thread, device), grown on demand up to LZF_GPU_SCRATCH_MB
- * (default 24 GiB: 1 M values of 8 KiB in one chunk; larger batches run in chunks).  A batch on another stream
+ * (default 40 GiB: 1 M values of 8 KiB or 256 K of 64 KiB in one chunk; larger batches run in chunks).  A batch on another stream
  * than the previous user waits for that user's kernels first. */
 struct Scratch {
     void *p = nullptr;
@@ -86,7 +86,7 @@ struct Scratch {
 size_t scratch_limit()
 {
     const char *e = getenv("LZF_GPU_SCRATCH_MB");
-    unsigned long long mb = e ? strtoull(e, nullptr, 10) : 24576ull;
+    unsigned long long mb = e ? strtoull(e, nullptr, 10) : 40960ull;
     if (mb < 1) mb = 1;
     return (size_t)mb << 20;
 }
@@ -141,11 +141,13 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s)
  * tools/crossover.py measured the crossover near 160 k values of 4 KiB,
  * near 48 k values of 8 KiB (window64 is 2.2x slower per byte there) and
  * near 160 k values of 16 KiB (mixed entropy: 86.0 vs 82.0 ms at 128 K,
- * 136.8 vs 163.8 ms at 256 K) */
+ * 136.8 vs 163.8 ms at 256 K) and near 96 k values of 64 KiB (sentence
+ * text: 172.4 vs 164.9 ms at 64 K, 261.6 vs 327.6 ms at 128 K) */
 uint32_t lane_min_count(uint32_t max_len)
 {
     const char *e = getenv("LZF_GPU_LANE_MIN");
     if (e) return (uint32_t)strtoul(e, nullptr, 10);
+    if (max_len > 16384u) return 98304u;
     return (max_len > 4096u && max_len <= 8192u) ? 49152u : 163840u;
 }
 
@@ -155,7 +157,7 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
     case GEN_SERIAL: return lzf_launch_compress_serial(b, s);
     case GEN_WINDOW: return lzf_launch_compress(b, s);
     default:
-        /* batches with values past 16 KiB, and small batches, go to the window
+        /* batches with values past 64 KiB, and small batches, go to the window
          * generation: the lane parse runs one value per lane, so its time has a
          * floor of one whole value's parse (~5 ms); below ~160 k values one
          * wave per value finishes first (tools/crossover.py) */
@@ -621,10 +623,11 @@ const char *lzf_gpu_kernel_info(void)
             lzf_decompress_kernel_name();
         break;
     default:
-        s = std::string("compress=lane(cand+parse; window64 past 16 KiB or below ") +
+        s = std::string("compress=lane(cand+parse; window64 past 64 KiB or below ") +
             std::to_string(lane_min_count(4096u)) + " values of <= 4 KiB / " +
             std::to_string(lane_min_count(8192u)) + " of <= 8 KiB / " +
-            std::to_string(lane_min_count(16384u)) + " of <= 16 KiB) decompress=" +
+            std::to_string(lane_min_count(16384u)) + " of <= 16 KiB / " +
+            std::to_string(lane_min_count(65536u)) + " of <= 64 KiB) decompress=" +
             (lane_decoder() ? "lane" : lzf_decompress_kernel_name());
         break;
     }

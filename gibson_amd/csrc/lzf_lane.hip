@@ -566,20 +566,36 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
  * sentence text 473 vs 676 ms.  With u32 links (2 values per CU) it was
  * 702 / 523 / 549 ms. */
 #define KR_MAXN 16384u
+#define KR64_MAXN 65536u
 #ifndef KR_WIN
 #define KR_WIN  2u
 #endif
-template <uint32_t WIN>
+template <uint32_t MAXN, uint32_t WIN>
 __global__ __launch_bounds__(64) void lzf_cand_ring_kernel(LzfBatch bt, LzfLaneScratch sc)
 {
     constexpr uint32_t IDB = 4u, IDM = 15u, BUCKETS = 4096u, RING = LZF_WINDOW;
     constexpr uint32_t T0 = 0u, T1 = 64u, T2 = 128u, TN = 144u;   /* digits as at 4 KiB */
-    constexpr uint32_t PF = KR_MAXN / 1024u;
+    /* values past 16 KiB stream their bytes through a 16 KiB LDS ring in 1 KiB
+     * chunks, one chunk in flight in registers: a step reads positions from
+     * P - 8192 (the window) to P + 64*WIN + 12, and a chunk is stored only
+     * once P + 64*WIN + 16 passes the bytes staged, so it never overwrites a
+     * byte the window still reaches */
+    constexpr bool STREAM = MAXN > KR_MAXN;
+    constexpr uint32_t RB = 16384u, WM = RB / 4u - 1u;
+    constexpr uint32_t PF = STREAM ? 1u : MAXN / 1024u;
     __shared__ __attribute__((aligned(16))) uint32_t H[BUCKETS];
     __shared__ uint16_t E[RING];
     __shared__ uint16_t S[64u * WIN];
-    __shared__ __attribute__((aligned(16))) uint32_t Bw[KR_MAXN / 4u + 4u];
+    __shared__ __attribute__((aligned(16))) uint32_t Bw[STREAM ? RB / 4u : MAXN / 4u + 4u];
     __shared__ unsigned long long T[WIN][TN];
+    const auto rd4 = [&](uint32_t x) -> uint32_t {
+        if constexpr (STREAM) {
+            const uint32_t w = x >> 2;
+            return __builtin_amdgcn_alignbyte(Bw[(w + 1u) & WM], Bw[w & WM], x & 3u);
+        } else {
+            return ks_rd4(Bw, x);
+        }
+    };
     const uint32_t lane = threadIdx.x;
     const unsigned long long mine = 1ull << lane, below = mine - 1ull;
     uint32_t v = blockIdx.x;
@@ -587,7 +603,7 @@ __global__ __launch_bounds__(64) void lzf_cand_ring_kernel(LzfBatch bt, LzfLaneS
     for (uint32_t k = lane; k < WIN * TN; k += 64u) (&T[0][0])[k] = 0ull;
     uint4 pf[PF];
     uint32_t pn = bt.in_len[v];
-    {
+    if (!STREAM) {
         const uint8_t *s0 = bt.in + bt.in_off[v];
 #pragma unroll
         for (uint32_t k = 0; k < PF; k++) {
@@ -598,10 +614,17 @@ __global__ __launch_bounds__(64) void lzf_cand_ring_kernel(LzfBatch bt, LzfLaneS
     while (v < bt.count) {
         const uint32_t n = pn;
         uint16_t *cand = sc.cand + (uint64_t)v * sc.cstride;
+        const uint8_t *src = bt.in + bt.in_off[v];
+        uint32_t L = 0u;                           /* STREAM: bytes staged in the ring */
+        if (!STREAM) {
 #pragma unroll
-        for (uint32_t k = 0; k < PF; k++) ((uint4 *)Bw)[64u * k + lane] = pf[k];
+            for (uint32_t k = 0; k < PF; k++) ((uint4 *)Bw)[64u * k + lane] = pf[k];
+        } else {                                   /* the first chunk */
+            pf[0] = 16u * lane < n ? ln_ld16_safe(src + 16u * lane, n - 16u * lane) : make_uint4(0, 0, 0, 0);
+        }
         const uint32_t vn = v + gridDim.x;
-        if (vn < bt.count) {                       /* next value's bytes, in flight */
+        if (vn < bt.count) pn = bt.in_len[vn];
+        if (!STREAM && vn < bt.count) {            /* next value's bytes, in flight */
             pn = bt.in_len[vn];
             const uint8_t *s1 = bt.in + bt.in_off[vn];
 #pragma unroll
@@ -615,13 +638,20 @@ __global__ __launch_bounds__(64) void lzf_cand_ring_kernel(LzfBatch bt, LzfLaneS
             ln_wave_fence();
             const uint32_t np = n - 2u;               /* positions 0 .. n-3 */
             for (uint32_t P = 0; P < np; P += 64u * WIN) {
+                if (STREAM && L < n && L < P + 64u * WIN + 16u) {
+                    ((uint4 *)Bw)[((L >> 4) + lane) & (RB / 16u - 1u)] = pf[0];
+                    L += 1024u;
+                    const uint32_t at = L + 16u * lane;
+                    pf[0] = at < n ? ln_ld16_safe(src + at, n - at) : make_uint4(0, 0, 0, 0);
+                    ln_wave_fence();
+                }
                 uint32_t p[WIN], m[WIN], tri[WIN];
                 bool act[WIN];
 #pragma unroll
                 for (uint32_t j = 0; j < WIN; j++) {
                     p[j] = P + 64u * j + lane;
                     act[j] = p[j] < np;
-                    tri[j] = ks_rd4(Bw, act[j] ? p[j] : 0u);
+                    tri[j] = rd4(act[j] ? p[j] : 0u);
                 }
 #pragma unroll
                 for (uint32_t j = 0; j < WIN; j++) {
@@ -700,7 +730,7 @@ __global__ __launch_bounds__(64) void lzf_cand_ring_kernel(LzfBatch bt, LzfLaneS
                         if (cp[j]) {
                             const uint32_t y = cp[j] - 1u;
                             const uint32_t e = KR_LINK(y);
-                            const uint32_t ty = ks_rd4(Bw, y);
+                            const uint32_t ty = rd4(y);
                             if (ci[j] == (m[j] & 7u) && ln_mix(ln_slot(ty)) == m[j]) {
                                 q1[j] = cp[j];
                                 cp[j] = 0u;
@@ -722,8 +752,8 @@ __global__ __launch_bounds__(64) void lzf_cand_ring_kernel(LzfBatch bt, LzfLaneS
                     uint32_t w = 0u;
                     if (q1[j] > 1u) {                    /* q = q1 - 1 > 0, p - q - 1 < 8192 */
                         const uint32_t q = q1[j] - 1u;
-                        const uint32_t x0 = tri[j] ^ ks_rd4(Bw, q);
-                        const uint32_t x1 = ks_rd4(Bw, p[j] + 4u) ^ ks_rd4(Bw, q + 4u);
+                        const uint32_t x0 = tri[j] ^ rd4(q);
+                        const uint32_t x1 = rd4(p[j] + 4u) ^ rd4(q + 4u);
                         const uint64_t xx = ((uint64_t)x1 << 32) | x0;
                         uint32_t k = xx ? (uint32_t)__builtin_ctzll(xx) >> 3 : 8u;
                         const uint32_t avail = n - p[j];
@@ -1485,11 +1515,9 @@ size_t lzf_lane_scratch_per_value(uint32_t max_len)
     return (size_t)(lane_cstride(max_len) * 2u + lane_bstride(max_len) * 4u);
 }
 
-/* The default lane path takes the small classes only (values <= 16 KiB;
- * LZF_GPU_LANE_RING=0 stops it at 8 KiB): on longer values the window
- * generation is faster today;
- * LZF_GPU_LANE_MID=1 routes values up to 64 KiB through the mid-class
- * kernels as well. */
+/* The default lane path takes the small and ring classes (values <= 64 KiB;
+ * LZF_GPU_LANE_RING=0 stops it at 8 KiB, and LZF_GPU_LANE_MID=1 then routes
+ * values up to 64 KiB through the mid-class kernels). */
 static bool lane_ring_enabled()
 {
     const char *r = getenv("LZF_GPU_LANE_RING");     /* "0" turns the ring class off */
@@ -1499,7 +1527,7 @@ static bool lane_ring_enabled()
 bool lzf_lane_compress_supported(uint32_t max_len)
 {
     if (max_len <= KS8_MAXN) return true;
-    if (max_len <= KR_MAXN && lane_ring_enabled()) return true;
+    if (max_len <= KR64_MAXN && lane_ring_enabled()) return true;
     const char *e = getenv("LZF_GPU_LANE_MID");
     return max_len <= KM_MAXN && e && *e == '1';
 }
@@ -1534,10 +1562,11 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
     }
     /* the small-class kernel is persistent: as many one-wave workgroups as
      * stay resident (LDS-bound), each walking the batch */
+    const bool ring = b.max_len > KS8_MAXN && b.max_len <= KR64_MAXN && lane_ring_enabled();
     const void *small_fn = b.max_len <= KS_MAXN    ? (const void *)lzf_cand_small_kernel<4u, KS_MAXN, KS_WIN>
                            : b.max_len <= KS8_MAXN ? (const void *)lzf_cand_small_kernel<3u, KS8_MAXN, KS8_WIN>
-                                                   : (const void *)lzf_cand_ring_kernel<KR_WIN>;
-    const bool ring = b.max_len > KS8_MAXN && b.max_len <= KR_MAXN && lane_ring_enabled();
+                           : b.max_len <= KR_MAXN  ? (const void *)lzf_cand_ring_kernel<KR_MAXN, KR_WIN>
+                                                   : (const void *)lzf_cand_ring_kernel<KR64_MAXN, KR_WIN>;
     uint32_t small_grid = 256u * 8u;
     {
         int dev = 0, cus = 0;
@@ -1586,7 +1615,10 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
             hipLaunchKernelGGL((lzf_cand_small_kernel<3u, KS8_MAXN, KS8_WIN>), dim3(g), dim3(64), 0, s, c, sc[h]);
         } else if (ring) {
             const uint32_t g = cnt < small_grid ? cnt : small_grid;
-            hipLaunchKernelGGL((lzf_cand_ring_kernel<KR_WIN>), dim3(g), dim3(64), 0, s, c, sc[h]);
+            if (b.max_len <= KR_MAXN)
+                hipLaunchKernelGGL((lzf_cand_ring_kernel<KR_MAXN, KR_WIN>), dim3(g), dim3(64), 0, s, c, sc[h]);
+            else
+                hipLaunchKernelGGL((lzf_cand_ring_kernel<KR64_MAXN, KR_WIN>), dim3(g), dim3(64), 0, s, c, sc[h]);
         } else {
             hipLaunchKernelGGL(lzf_cand_mid_kernel, dim3(cnt), dim3(64), 0, s, c, sc[h]);
         }

@@ -169,6 +169,7 @@ def test_lane_mid_class(oracle, monkeypatch):
     from tests.gpu_batch import gpu_compress
     monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
     monkeypatch.setenv("LZF_GPU_LANE_MID", "1")
+    monkeypatch.setenv("LZF_GPU_LANE_RING", "0")
     rnd = random.Random(21)
     vals = [synth(rnd.randrange(6), 0x5EED00F0, i, rnd.randint(1, 20000)) for i in range(300)]
     caps = [rnd.choice([max(1, len(v) - 4), len(v) + len(v) // 16 + 64]) for v in vals]
@@ -177,15 +178,17 @@ def test_lane_mid_class(oracle, monkeypatch):
 
 @pytest.mark.parametrize("align", [16, 3])
 def test_lane_ring_class(oracle, monkeypatch, align):
-    # the 16 KiB ring form of the cand kernel (values 8-16 KiB): links
-    # kept for the last 8 KiB of positions, window tests on heads and links
+    # the ring form of the cand kernel (values 8-64 KiB): links kept for the
+    # last 8 KiB of positions, window tests on heads and links, and past
+    # 16 KiB the bytes streamed through an LDS ring
     from tests.gpu_batch import gpu_compress, gpu_decompress
     monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
     monkeypatch.setenv("LZF_GPU_LANE_RING", "1")
     rnd = random.Random(33 + align)
     vals = []
     for i in range(1500):
-        n = rnd.choice([rnd.randint(1, 700), rnd.randint(8000, 16384), 16384])
+        n = rnd.choice([rnd.randint(1, 700), rnd.randint(8000, 16384), 16384,
+                         rnd.randint(16385, 65536), 65536])
         v = synth(rnd.randrange(6), 0x5EED00F8, i, n)
         if rnd.random() < 0.1:
             v = bytes(rnd.choice(b"abc") for _ in range(n))
@@ -233,6 +236,7 @@ def test_lane_order_repair_path(oracle, monkeypatch):
     monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
     monkeypatch.setenv("LZF_GPU_LANE_FORCE_FIX", "1")
     monkeypatch.setenv("LZF_GPU_LANE_MID", "1")
+    monkeypatch.setenv("LZF_GPU_LANE_RING", "0")
     rnd = random.Random(3)
     for nmax in (4096, 20000):
         vals = [synth(rnd.randrange(6), 0x5EED00D0, i, rnd.randint(1, nmax)) for i in range(200)]
@@ -240,13 +244,13 @@ def test_lane_order_repair_path(oracle, monkeypatch):
         assert gpu_compress(vals, caps) == [oracle.compress(v, c) for v, c in zip(vals, caps)]
 
 
-@pytest.mark.parametrize("nmax", [4096, 8192, 9000, 16384])
+@pytest.mark.parametrize("nmax", [4096, 8192, 9000, 16384, 65536])
 def test_random_differential(oracle, generation, nmax, monkeypatch):
     # nmax 8192: the batch fits the non-wrapping ring/chain kernel; 9000:
     # the wrapping one (the kernel is chosen per batch from max_len); 16384
     # takes the lane generation's ring class
     from tests.gpu_batch import gpu_compress, gpu_decompress
-    if nmax == 16384:
+    if nmax >= 16384:
         monkeypatch.setenv("LZF_GPU_LANE_RING", "1")
     rnd = random.Random(7 + nmax)
     vals, caps = [], []

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Compress time by batch size for the lane and window generations: where
-does the lane generation start to pay?  usage: crossover.py [KIND N]
+does the lane generation start to pay?  usage: crossover.py [KIND N [MAX_COUNT]]
 (default json4k: 1 4096).  The lane parse runs
 one value per lane, so a small batch leaves the GPU mostly idle while each
 lane walks its whole value."""
@@ -15,7 +15,7 @@ import gibson_amd  # noqa: E402
 
 kind = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
-N = 1 << 20
+N = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 20
 os.environ["LZF_GPU_LANE_MIN"] = "0"
 dev = torch.device("cuda")
 src = torch.empty(N * n, dtype=torch.uint8, device=dev)
@@ -43,4 +43,6 @@ def t(count, gen):
 
 
 for count in (1 << 10, 1 << 12, 1 << 14, 1 << 16, 1 << 17, 1 << 18, 1 << 19, 1 << 20):
+    if count > N:
+        break
     print(f"{count:8d} values: lane {t(count, 'lane'):8.2f} ms   window {t(count, 'window'):8.2f} ms", flush=True)
