@@ -30,8 +30,35 @@
 #ifndef CD_ROUND
 #define CD_ROUND   128              /* input bytes whose token starts one round covers: 64 or 128 */
 #endif
-#define CD_IN_RING 4096u
-#define CD_OUT_MAX 16384u
+/* input ring: a round reads [base, base + CD_ROUND + 33); staging runs in
+ * CD_STAGE-byte pieces (one 16-byte load per lane) when the round's reach
+ * passes the bytes staged, so a piece overwrites only bytes more than
+ * CD_IN_RING - CD_STAGE - 2 * CD_ROUND before base.  A small ring keeps the
+ * kernel's LDS small: residency, not bandwidth, bounds this decoder */
+#ifndef CD_IN_RING
+#define CD_IN_RING 1024u
+#endif
+#define CD_STAGE   512u
+/* output window ring: back-references reach at most 8192 bytes back
+ * (src/lzf_d.c:95, off < 8192), and a group reads all its sources before it
+ * writes its 64 bytes, so a ring of 8 KiB suffices: the slots a group
+ * overwrites (o - 8192) are read, if at all, by that group alone */
+#ifndef CD_OUT_MAX
+#define CD_OUT_MAX 8192u
+#endif
+
+/* 16 bytes from p, of which `avail` (< 16: the rest reads as zero) exist */
+__device__ __forceinline__ uint4 cd_ld16(const uint8_t *p, uint32_t avail)
+{
+    uint4 v;
+    if (avail >= 16u) {
+        __builtin_memcpy(&v, p, 16);
+        return v;
+    }
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t k = 0; k < avail; k++) w[k >> 2] |= (uint32_t)p[k] << (8u * (k & 3u));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
 
 __device__ __forceinline__ uint64_t cd_lt(uint32_t i)
 {
@@ -109,11 +136,11 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
          * round and their literal payloads, <= CD_ROUND - 1 + 33 bytes) */
         uint32_t need = base + 2u * CD_ROUND;
         if (need > avail) need = avail;
-        if (loaded < need) {
-            uint32_t to = loaded + 2048u;
-            if (to < need) to = need;
+        if (loaded < need) {                 /* need - loaded <= CD_ROUND + 33 < CD_STAGE */
+            uint32_t to = loaded + CD_STAGE;
             if (to > avail) to = avail;
-            for (uint32_t x = loaded + lane; x < to; x += CD_LANES) inr[x & imask] = src[x];
+            const uint32_t x = loaded + 16u * lane;   /* loaded is a multiple of 16 here */
+            if (x < to) *(uint4 *)(inr + (x & imask)) = cd_ld16(src + x, to - x);
             loaded = to;
             cd_fence();
         }
