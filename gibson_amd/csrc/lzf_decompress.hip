@@ -32,13 +32,15 @@
 #endif
 /* input ring: a round reads [base, base + CD_ROUND + 33); staging runs in
  * CD_STAGE-byte pieces (one 16-byte load per lane) when the round's reach
- * passes the bytes staged, so a piece overwrites only bytes more than
- * CD_IN_RING - CD_STAGE - 2 * CD_ROUND before base.  A small ring keeps the
- * kernel's LDS small: residency, not bandwidth, bounds this decoder */
+ * passes base + 2 * CD_ROUND (loaded < base + 2 * CD_ROUND), so a piece
+ * overwrites only bytes before loaded - CD_IN_RING + CD_STAGE < base, which
+ * no later round reads.  A small ring keeps the kernel's LDS small:
+ * residency, not bandwidth, bounds this decoder */
 #ifndef CD_IN_RING
-#define CD_IN_RING 1024u
+#define CD_IN_RING 512u
 #endif
-#define CD_STAGE   512u
+#define CD_STAGE   (CD_IN_RING / 2u)
+static_assert(CD_STAGE >= 2u * CD_ROUND && CD_STAGE <= 16u * CD_LANES, "one staging piece per round");
 /* output window ring: back-references reach at most 8192 bytes back
  * (src/lzf_d.c:95, off < 8192), and a group reads all its sources before it
  * writes its 64 bytes, so a ring of 8 KiB suffices: the slots a group
@@ -136,7 +138,7 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
          * round and their literal payloads, <= CD_ROUND - 1 + 33 bytes) */
         uint32_t need = base + 2u * CD_ROUND;
         if (need > avail) need = avail;
-        if (loaded < need) {                 /* need - loaded <= CD_ROUND + 33 < CD_STAGE */
+        if (loaded < need) {                 /* need - loaded <= CD_ROUND + 33 <= CD_STAGE */
             uint32_t to = loaded + CD_STAGE;
             if (to > avail) to = avail;
             const uint32_t x = loaded + 16u * lane;   /* loaded is a multiple of 16 here */
@@ -311,7 +313,7 @@ hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s)
 {
     uint32_t ring = 256u;
     while (ring < b.max_len && ring < CD_OUT_MAX) ring <<= 1;
-    const size_t lds = CD_IN_RING + ring + 2u * CD_LANES * 4u;
+    const size_t lds = CD_IN_RING + ring + CD_LANES * 4u;     /* + the 64 marks */
     hipError_t e = hipFuncSetAttribute((const void *)lzf_decompress_tokpar_kernel,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
