@@ -110,7 +110,12 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s)
             S.p = nullptr;
             S.cap = 0;
         }
-        e = hipMalloc(&S.p, want);
+        /* short of device memory: a smaller scratch only means more chunks */
+        const size_t least = 2 * per + 1024;
+        while ((e = hipMalloc(&S.p, want)) != hipSuccess && want > least) {
+            (void)hipGetLastError();
+            want = want / 2 > least ? want / 2 : least;
+        }
         if (e != hipSuccess) return e;
         S.cap = want;
         S.used = false;

@@ -202,6 +202,24 @@ def test_lane_ring_class(oracle, monkeypatch, align):
     assert gpu_decompress(streams, [len(v) for v in origs]) == [(v, 0) for v in origs]
 
 
+@pytest.mark.parametrize("nmax", [4096, 8192, 16384, 65536])
+def test_lane_scratch_chunks(oracle, monkeypatch, nmax):
+    # a small compress scratch cap runs the lane kernels over many chunks;
+    # the scratch is per host thread, so a fresh thread sees the cap
+    import threading
+    from tests.gpu_batch import gpu_compress
+    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.setenv("LZF_GPU_SCRATCH_MB", "4")
+    rnd = random.Random(nmax)
+    vals = [synth(rnd.randrange(6), 0x5EED00FA, i, rnd.randint(1, nmax)) for i in range(400)]
+    caps = [max(1, len(v) - 4) for v in vals]
+    out = {}
+    th = threading.Thread(target=lambda: out.setdefault("r", gpu_compress(vals, caps, align=3)))
+    th.start()
+    th.join()
+    assert out["r"] == [oracle.compress(v, c) for v, c in zip(vals, caps)]
+
+
 @pytest.mark.parametrize("align", [16, 3])
 def test_wave_parse(oracle, monkeypatch, align):
     # the wave form of the parse kernel (64 positions per step, opt-in):
