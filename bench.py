@@ -8,11 +8,18 @@ policy of src/query.c:385) followed by lzf_gpu_decompress_batch of the
 results (out_len = n).  Values that do not compress are not decoded (as in
 the server, src/query.c:393-397).
 
-Default workload = BASELINE.json configs[1]: 1 M x 4 KiB JSON-like values per
-GPU.  Multi-GPU: one process per GPU (torchrun), values sharded round-robin
-(value i -> rank i mod N); no data-path collective, only a
-barrier and a max-over-ranks of the timings.  Weak scaling: every rank owns
-`count` values.
+Default workload = BASELINE.json configs[2]: 256 K x 64 KiB sentence-bank
+text values per GPU (the north star's 64 KiB target and the largest
+single-GPU compress+decompress config).  Multi-GPU: one process per GPU,
+values sharded round-robin (value i -> rank i mod N); no
+data-path collective, only a barrier and a max-over-ranks of the timings.
+Weak scaling by default (every rank owns `count` values); `--total T` is the
+strong-scaling mode (T values over all ranks, e.g. BASELINE configs[4]:
+--workload mixed16k --total 4194304).
+
+`--gpus N` with N > 1 and no torchrun environment re-launches this script
+under torch.distributed.run with N ranks (a child process, started before
+any GPU call); under torchrun, --gpus must equal WORLD_SIZE.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), including
 "roofline" for the dominant kernel (HIP events on the launch stream) and
@@ -54,44 +61,96 @@ DESCR = {
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs (ranks) on this node; default 1")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--mode", default="roundtrip", choices=("roundtrip", "decompress"),
                     help="roundtrip = the headline (compress+decompress); decompress = "
                          "BASELINE configs[3], decode of pre-compressed blocks only")
     ap.add_argument("--workload", default="", choices=[""] + sorted(WORKLOADS),
-                    help="default: json4k (roundtrip), text8k (decompress)")
+                    help="default: text64k (roundtrip, BASELINE configs[2]), text8k (decompress)")
     ap.add_argument("--count", type=int, default=0, help="values per GPU (default: workload's)")
+    ap.add_argument("--total", type=int, default=0,
+                    help="strong scaling: values over all ranks (rank r takes values r, r+N, ...)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-count", type=int, default=0, help="CPU baseline sample values")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (default: the cores this process may run on)")
     return ap.parse_args()
 
 
-def cpu_baseline(kind, seed, n, count, threads, decode_only=False):
-    """Time the CPU codec on a bounded sample (checker/baseline only)."""
+def launch_ranks(a):
+    """--gpus N without a torchrun environment: run N ranks as a child
+    torch.distributed.run (this process has not touched the GPU) and exit
+    with its status.  Under torchrun, --gpus must match WORLD_SIZE."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if a.gpus is not None and a.gpus != int(world):
+            sys.exit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
+        return
+    if a.gpus is None or a.gpus <= 1:
+        return
+    import socket
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
+def cpu_cores():
+    """Cores this process may run on (the affinity set, i.e. nproc)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def _cpu_run(kind, seed, n, count, threads, reps):
     ref = os.path.join(ROOT, "oracle", "_ref", "cpu_bench_ref")
     port = os.path.join(ROOT, "oracle", "cpu_bench")
     exe = ref if os.path.exists(ref) else port
     if not os.path.exists(exe):
         return None
-    out = subprocess.run([exe, str(kind), str(n), str(count), str(threads), hex(seed), "5"],
-                         capture_output=True, text=True, timeout=600)
+    out = subprocess.run([exe, str(kind), str(n), str(count), str(threads), hex(seed), str(reps)],
+                         capture_output=True, text=True, timeout=900,
+                         env=dict(os.environ, OMP_NUM_THREADS=str(threads)))
     if out.returncode != 0:
         return {"error": out.stderr.strip()[-200:]}
-    r = json.loads(out.stdout)
-    return {
-        "value": round(r["decompress_GBps" if decode_only else "roundtrip_GBps"], 4),
+    return json.loads(out.stdout)
+
+
+def cpu_baseline(kind, seed, n, count, threads, decode_only=False):
+    """Time the CPU codec (the reference compiled by oracle/Makefile) on
+    bounded samples of the workload (checker/baseline only): on all the
+    cores this process may run on (`threads`, one value per OpenMP thread)
+    and on one core."""
+    key = "decompress_GBps" if decode_only else "roundtrip_GBps"
+    r = _cpu_run(kind, seed, n, count, threads, 5)
+    if r is None or "error" in r:
+        return r
+    cnt1 = max(16, min(count, (96 << 20) // n))
+    r1 = _cpu_run(kind, seed, n, cnt1, 1, 3)
+    what = "decompress of the reference-compressed values" if decode_only else "compress+decompress"
+    out = {
+        "value": round(r[key], 4),
         "unit": "GB/s",
         "cores": threads,
         "kind": r["kind"],
-        "sample": f"{count} values x {n} B (first {count} of the workload's value indices), "
-                  f"{'decompress of the reference-compressed values' if decode_only else 'compress+decompress'}, median of 5 after 1 warm-up, one value per OpenMP "
-                  f"thread; compress {r['compress_GBps']:.3f} GB/s, decompress "
-                  f"{r['decompress_GBps']:.3f} GB/s, ratio {r['comp_bytes'] / r['in_bytes']:.4f}",
+        "sample": f"{count} values x {n} B (the workload's first {count} value indices), {what}, "
+                  f"median of 5 after 1 warm-up, one value per OpenMP thread on {threads} threads; "
+                  f"compress {r['compress_GBps']:.3f} GB/s, decompress {r['decompress_GBps']:.3f} GB/s, "
+                  f"ratio {r['comp_bytes'] / r['in_bytes']:.4f}",
         "cpu": _cpu_model(),
     }
+    if r1 and "error" not in r1:
+        out["value_1core"] = round(r1[key], 4)
+        out["sample_1core"] = (f"{cnt1} values x {n} B, median of 3 after 1 warm-up, 1 thread; "
+                               f"compress {r1['compress_GBps']:.4f} GB/s, "
+                               f"decompress {r1['decompress_GBps']:.4f} GB/s")
+    return out
 
 
 def _traffic(workload, kernel, count):
@@ -118,6 +177,7 @@ def _cpu_model():
 
 def main():
     a = parse()
+    launch_ranks(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -128,12 +188,14 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
     if not a.workload:
-        a.workload = "text8k" if a.mode == "decompress" else "json4k"
+        a.workload = "text8k" if a.mode == "decompress" else "text64k"
     cfg_idx, kind, seed, n, count = WORKLOADS[a.workload]
     if a.mode == "decompress" and a.workload == "text8k":
         count = 8 << 20                                  # BASELINE configs[3]: 8 M blocks
     if a.count:
         count = a.count
+    if a.total:                                          # strong scaling: rank's round-robin share
+        count = (a.total - rank + world - 1) // world
     if a.mode == "decompress":
         return main_decompress(a, world, rank, dev, cfg_idx, kind, seed, n, count)
 
@@ -221,12 +283,13 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(sec_per_step * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if a.total else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": DESCR[a.workload],
+                "workload": DESCR[a.workload] if not a.total else
+                            f"{a.total} x {n // 1024} KiB values over all ranks ({DESCR[a.workload]})",
                 "baseline_config": cfg_idx,
                 "values_per_gpu": count,
                 "value_bytes": n,
@@ -251,8 +314,8 @@ def main():
             },
         }
         if world == 1 and not a.no_cpu:
-            threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-            cnt = a.cpu_count or min(count, max(64, (4 << 30) // n))
+            threads = a.cpu_threads or cpu_cores()
+            cnt = a.cpu_count or min(count, max(4 * threads, (4 << 30) // n))
             line["cpu_baseline"] = cpu_baseline(kind, seed, n, cnt, threads)
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -372,8 +435,8 @@ def main_decompress(a, world, rank, dev, cfg_idx, kind, seed, n, count):
             },
         }
         if world == 1 and not a.no_cpu:
-            threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-            cnt = a.cpu_count or min(count, max(64, (4 << 30) // n))
+            threads = a.cpu_threads or cpu_cores()
+            cnt = a.cpu_count or min(count, max(4 * threads, (4 << 30) // n))
             line["cpu_baseline"] = cpu_baseline(kind, seed, n, cnt, threads, decode_only=True)
         print(json.dumps(line), flush=True)
     if world > 1:
