@@ -33,7 +33,7 @@ hipError_t lzf_launch_decompress_serial(const LzfBatch &b, hipStream_t s);
 
 namespace {
 
-enum KernelGen { GEN_LANE = 0, GEN_WINDOW = 1, GEN_SERIAL = 2 };
+enum KernelGen { GEN_TABLE = 0, GEN_LANE = 1, GEN_WINDOW = 2, GEN_SERIAL = 3 };
 
 /* LZF_GPU_KERNEL picks the kernel generation, read per launch so one process
  * can A/B them: "lane" (default; one lane per value, lzf_lane.hip),
@@ -45,7 +45,8 @@ KernelGen kernel_gen()
     const char *e = getenv("LZF_GPU_KERNEL");
     if (e && !strcmp(e, "serial")) return GEN_SERIAL;
     if (e && !strcmp(e, "window")) return GEN_WINDOW;
-    return GEN_LANE;
+    if (e && !strcmp(e, "lane")) return GEN_LANE;
+    return GEN_TABLE;
 }
 
 bool device_ok(int dev)
@@ -83,24 +84,34 @@ struct Scratch {
     hipEvent_t pev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
-size_t scratch_limit()
+/* Scratch cap: LZF_GPU_SCRATCH_MB if set, else half of the device memory
+ * free when the scratch grows (at least 1 GiB): a whole BASELINE batch
+ * (256 K x 64 KiB: 67 GiB of records) then runs as one chunk, and a caller
+ * that holds most of the device still gets chunked, not refused. */
+size_t scratch_limit(size_t held)
 {
     const char *e = getenv("LZF_GPU_SCRATCH_MB");
-    unsigned long long mb = e ? strtoull(e, nullptr, 10) : 40960ull;
-    if (mb < 1) mb = 1;
-    return (size_t)mb << 20;
+    if (e) {
+        unsigned long long mb = strtoull(e, nullptr, 10);
+        if (mb < 1) mb = 1;
+        return (size_t)mb << 20;
+    }
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return (size_t)40 << 30;
+    size_t lim = (fr + held) / 2;
+    return lim > ((size_t)1 << 30) ? lim : ((size_t)1 << 30);
 }
 
-hipError_t lane_compress(const LzfBatch &b, hipStream_t s)
+hipError_t lane_compress(const LzfBatch &b, hipStream_t s, bool table)
 {
     static thread_local Scratch per_dev[64];
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     Scratch &S = per_dev[dev & 63];
-    const size_t per = lzf_lane_scratch_per_value(b.max_len);
+    const size_t per = table ? lzf_table_scratch_per_value(b.max_len) : lzf_lane_scratch_per_value(b.max_len);
     size_t want = per * (size_t)b.count + 512;
-    const size_t lim = scratch_limit();
+    const size_t lim = scratch_limit(S.cap);
     if (want > lim) want = lim;
     if (want < 2 * per + 1024) want = 2 * per + 1024;     /* two pipeline halves */
     if (S.cap < want) {
@@ -133,8 +144,9 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s)
         for (int k = 0; k < 4; k++)
             if ((e = hipEventCreateWithFlags(&S.pev[k], hipEventDisableTiming)) != hipSuccess) return e;
     }
-    e = lzf_launch_compress_lane(b, s, S.p, S.cap, (ff && *ff == '1') ? 1u : 0u,
-                                 pipe ? S.aux : nullptr, pipe ? S.pev : nullptr);
+    e = table ? lzf_launch_compress_table(b, s, S.p, S.cap)
+              : lzf_launch_compress_lane(b, s, S.p, S.cap, (ff && *ff == '1') ? 1u : 0u,
+                                         pipe ? S.aux : nullptr, pipe ? S.pev : nullptr);
     if (e != hipSuccess) return e;
     e = hipEventRecord(S.ev, s);
     S.last = s;
@@ -161,13 +173,17 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
     switch (kernel_gen()) {
     case GEN_SERIAL: return lzf_launch_compress_serial(b, s);
     case GEN_WINDOW: return lzf_launch_compress(b, s);
+    case GEN_LANE:
+        return (lzf_lane_compress_supported(b.max_len) && b.count >= lane_min_count(b.max_len))
+                   ? lane_compress(b, s, false)
+                   : lzf_launch_compress(b, s);
     default:
         /* batches with values past 64 KiB, and small batches, go to the window
-         * generation: the lane parse runs one value per lane, so its time has a
-         * floor of one whole value's parse (~5 ms); below ~160 k values one
+         * generation: the parse runs one value per lane, so its time has a
+         * floor of one whole value's parse (~5 ms); below the crossover one
          * wave per value finishes first (tools/crossover.py) */
-        return (lzf_lane_compress_supported(b.max_len) && b.count >= lane_min_count(b.max_len))
-                   ? lane_compress(b, s)
+        return (lzf_table_compress_supported(b.max_len) && b.count >= lane_min_count(b.max_len))
+                   ? lane_compress(b, s, true)
                    : lzf_launch_compress(b, s);
     }
 }
@@ -627,8 +643,16 @@ const char *lzf_gpu_kernel_info(void)
         s = std::string("compress=") + lzf_compress_kernel_name() + " decompress=" +
             lzf_decompress_kernel_name();
         break;
-    default:
+    case GEN_LANE:
         s = std::string("compress=lane(cand+parse; window64 past 64 KiB or below ") +
+            std::to_string(lane_min_count(4096u)) + " values of <= 4 KiB / " +
+            std::to_string(lane_min_count(8192u)) + " of <= 8 KiB / " +
+            std::to_string(lane_min_count(16384u)) + " of <= 16 KiB / " +
+            std::to_string(lane_min_count(65536u)) + " of <= 64 KiB) decompress=" +
+            (lane_decoder() ? "lane" : lzf_decompress_kernel_name());
+        break;
+    default:
+        s = std::string("compress=table(cand_table+parse_rec; window64 past 64 KiB or below ") +
             std::to_string(lane_min_count(4096u)) + " values of <= 4 KiB / " +
             std::to_string(lane_min_count(8192u)) + " of <= 8 KiB / " +
             std::to_string(lane_min_count(16384u)) + " of <= 16 KiB / " +

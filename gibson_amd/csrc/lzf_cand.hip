@@ -1,0 +1,734 @@
+/*
+ * lzf_cand.hip -- the "table" generation of the LZF compressor for gfx950
+ * (values of at most 64 KiB; larger values go to window64, lzf_compress.hip).
+ *
+ * The reference's greedy parse (src/lzf_c.c:145-274) is serial per value and
+ * its ref at a visited position p is the latest INSERTED position with p's
+ * 16-bit slot (src/lzf_c.c:147-149).  Inserted = every visited position plus
+ * the last two positions of each match (src/lzf_c.c:227-247); so the ref is
+ * the first position on the "same-slot chain" of p (p's nearest earlier
+ * same-slot position q1(p), then q1(q1(p)), ...) that the parse did not skip.
+ * Two kernels per batch:
+ *
+ *   1. lzf_cand_table_kernel -- position-parallel, one value per workgroup
+ *      of 8 waves (one per CU: the table is 128 KiB of LDS).  For every
+ *      position p: q1(p) and q2(p) = q1(q1(p)), each with how far its bytes
+ *      agree with p's (<= 8), packed in a u32 record in HBM scratch.
+ *      q1 comes from an exact direct-mapped table T[slot] -> latest position
+ *      (65536 x u16, the reference's own table size, src/lzfP.h:55), so
+ *      there are no bucket chains to walk on any data; q2 from a ring Q of
+ *      q1 over the last 8192 positions (a candidate farther back is outside
+ *      every window, src/lzf_c.c:153).  Per block of 512 positions:
+ *        A  each wave takes one window of 64 positions: bytes, slot, and the
+ *           same-slot lanes of the window (three 64-bit lane bitmaps in LDS,
+ *           keyed by the slot's digits; AND of the read-backs is exact);
+ *        B  wave w owns the slots with slot % 8 == w and does their table
+ *           reads and writes for the whole block, window by window -- one
+ *           wave's LDS operations execute in order, so T is read and written
+ *           in position order without any cross-wave ordering;
+ *        C  each wave takes its window again: q1, q2, agreement, record.
+ *
+ *   2. lzf_parse_rec_kernel -- the greedy parse and emission, ONE LANE PER
+ *      VALUE (a wave advances 64 values at once).  It keeps an inserted-
+ *      bitmap of its value (32 words in LDS, older words in HBM scratch) and
+ *      walks the chain only past skipped positions.  A record holds two
+ *      chain links, so a walk loads one record per two skipped candidates.
+ *
+ * Scratch per value: 4 B/position (records) + 1 bit/position (bitmap).
+ */
+#include <stdlib.h>
+
+#include "lzf_dev.h"
+
+/* record of position p: bits 0-12 off1 = p - q1 - 1, 13-15 code1,
+ * bits 16-28 off2 = p - q2 - 1, 29-31 code2.  Codes:
+ *   0     none (no earlier position with p's slot inside p's window, or only
+ *         position 0, which is never a ref: src/lzf_c.c:155 `ref > in_data`)
+ *   1     same slot, the three bytes differ (slot collision)
+ *   2..6  the bytes agree for exactly code + 1 bytes (3..7)
+ *   7     the bytes agree for >= 8 bytes                                   */
+#define RC_DIFF 1u
+#define RC_LONG 7u
+
+#define KT_WIN 7u                 /* windows of 64 positions per block = worker waves */
+#define KT_BLK (64u * KT_WIN)
+#define KT_THREADS (64u * (KT_WIN + 1u))
+#ifndef KT_PF
+#define KT_PF 4u                /* blocks of input bytes in flight per lane */
+#endif
+
+__device__ __forceinline__ uint32_t kt_code(uint32_t k)
+{
+    return k < 3u ? RC_DIFF : (k >= 8u ? RC_LONG : k - 1u);
+}
+
+
+__device__ __forceinline__ void kt_wave_fence()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+/* S entry of a position of the block */
+#define KS_ACT  (1u << 16)
+#define KS_PRED (1u << 17)     /* an earlier lane of its window has its slot */
+#define KS_LAST (1u << 18)     /* no later lane of its window has its slot */
+#define KS_PL   19u            /* bits 19-24: the nearest such earlier lane */
+
+/* the 8 bytes at pp: one branch-free 8-byte load for values of >= 8 bytes
+ * (the compiler then counts the loads in flight instead of draining them) */
+template <bool SMALL>
+__device__ __forceinline__ uint2 kt_ld8(const uint8_t *src, uint32_t n, uint32_t pp)
+{
+    if constexpr (SMALL) return pp < n ? dv_ld8_safe(src + pp, n - pp) : make_uint2(0u, 0u);
+    else return dv_ld8_clamped(src, n, pp);
+}
+
+/* how far the bytes at q agree with p's 8 bytes a (at most 8, at most
+ * avail = n - p); q < p */
+template <bool SMALL>
+__device__ __forceinline__ uint32_t kt_agree(uint2 a, const uint8_t *src, uint32_t n, uint32_t q,
+                                             uint32_t avail)
+{
+    const uint2 b = kt_ld8<SMALL>(src, n, q);
+    const uint64_t x = ((uint64_t)(a.y ^ b.y) << 32) | (uint64_t)(a.x ^ b.x);
+    const uint32_t k = x ? (uint32_t)__builtin_ctzll(x) >> 3 : 8u;
+    return k < avail ? k : avail;
+}
+
+/* Pipelined over blocks of KT_BLK = 7 windows (448 positions): wave 0 is the
+ * table wave, waves 1..7 are workers, and each step ends with ONE workgroup
+ * barrier.  Block k goes through
+ *   step k    A(k)   worker j: window j -- bytes, slot, same-slot lanes -> S[k%2]
+ *   step k+1  B(k)   table wave: T reads/writes of the 7 windows in order -> O[k%3]
+ *   step k+2  C1(k)  worker j: q1, q2 (O[k%3], O[(k-1)%3], Q); agreement loads issued
+ *   step k+3  C2(k)  worker j: agreement, record stored; Q <- O[k%3]
+ * so the agreement loads have a whole step to return.  Q(k) is written in
+ * step k+3: the slots it overwrites belong to positions 8192 before block k,
+ * which no C1 of block k+1 or later can reach (off < 8192). */
+/* -DKT_TIMING (diagnostic build): cycles per phase, summed over waves in
+ * kt_times[]: [0] table wave B, [1] table wave barrier, [2] C2, [3] C1,
+ * [4] A, [5] worker loads, [6] worker barrier, [7] steps */
+#ifdef KT_TIMING
+__device__ unsigned long long kt_times[16];
+extern "C" int lzf_gpu_debug_kt(unsigned long long *out16, int reset)
+{
+    hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(kt_times), sizeof(kt_times));
+    if (e == hipSuccess && reset) {
+        unsigned long long z[16] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(kt_times), z, sizeof(z));
+    }
+    return e == hipSuccess ? 0 : -2;
+}
+#define KT_T0() uint64_t kt_t = __builtin_amdgcn_s_memtime()
+#define KT_TM(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); kt_acc[i] += t_ - kt_t; kt_t = t_; } while (0)
+#else
+#define KT_T0() ((void)0)
+#define KT_TM(i) ((void)0)
+#endif
+
+struct KtLds {
+    uint16_t *T, *Q, *O;                 /* O: 3 buffers of KT_BLK */
+    uint32_t *S;                         /* S: 2 buffers of KT_BLK */
+    unsigned long long *Dw;              /* this worker's digit bitmaps */
+};
+
+template <uint32_t V> struct KtIc { static constexpr uint32_t value = V; };
+
+template <bool SMALL>
+__device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uint32_t n, uint32_t *rec)
+{
+    uint16_t *const T = L.T, *const Q = L.Q, *const O = L.O;
+    uint32_t *const S = L.S;
+    unsigned long long *const Dw = L.Dw;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const uint32_t j = w - 1u;                                 /* worker's window (w >= 1) */
+    const unsigned long long mine = 1ull << lane, below = mine - 1ull;
+    const uint32_t np = n - 2u;                                /* positions 0 .. n-3, src/lzf_c.c:145 */
+    const uint32_t nb = (np + KT_BLK - 1u) / KT_BLK;
+    /* worker: the 8 bytes of its position in the next KT_PF blocks are in
+     * flight; slot d holds the blocks = d (mod KT_PF), so the step loop is
+     * unrolled KT_PF times and no register rotates (a rotation would copy a
+     * register whose load is in flight, i.e. wait for it) */
+    uint2 pf[KT_PF], ak[KT_PF];
+#pragma unroll
+    for (uint32_t d = 0; d < KT_PF; d++) {
+        pf[d] = w ? kt_ld8<SMALL>(src, n, KT_BLK * d + 64u * j + lane) : make_uint2(0u, 0u);
+        ak[d] = make_uint2(0u, 0u);
+    }
+    /* the table starts empty for every value (position 0 = none: it is
+     * never a ref, and a candidate 0 decides like no candidate) */
+    for (uint32_t k = tid; k < LZF_SLOTS / 8u; k += KT_THREADS) ((uint4 *)T)[k] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    /* C1 -> C2 state of the worker's window */
+    uint32_t c_p = 0xFFFFFFFFu, c_q1 = 0u, c_q2 = 0u, c_avail = 0u;
+    uint2 c_a = make_uint2(0u, 0u), c_b1 = c_a, c_b2 = c_a;
+#ifdef KT_TIMING
+    uint64_t kt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+    const auto step = [&](auto ps, uint32_t t) {
+        constexpr uint32_t PS = decltype(ps)::value;             /* t % KT_PF */
+        KT_T0();
+        /* this step's global loads are issued unconditionally, by every
+         * wave, at the end: a load inside a branch leaves a register merge
+         * behind that waits for it */
+        uint32_t l1 = 0u, l2 = 0u;                               /* agreement loads of C1 */
+        const uint32_t lp = KT_BLK * (t + KT_PF) + 64u * j + lane;   /* input of block t + KT_PF */
+        if (w == 0u) {
+            /* ---- B(t-1): the table wave ------------------------------------- */
+            /* no exec masking: every lane reads T[slot] (a read the position
+             * does not need is ignored), a lane that is not its slot's last in
+             * the window writes its own dummy entry T[65536 + lane], and a
+             * lane with an earlier same-slot lane writes O from that lane */
+#ifdef KT_ABL_B
+            if (false) {
+#else
+            if (t >= 1u && t <= nb) {
+#endif
+                const uint32_t k = t - 1u, B = KT_BLK * k;
+                const uint32_t *Sk = S + KT_BLK * (k & 1u);
+                uint16_t *Ok = O + KT_BLK * (k % 3u);
+                uint32_t e[KT_WIN], tv[KT_WIN];
+#pragma unroll
+                for (uint32_t i = 0; i < KT_WIN; i++) e[i] = Sk[64u * i + lane];
+#pragma unroll
+                for (uint32_t i = 0; i < KT_WIN; i++) {             /* window order = position order */
+#if defined(KT_ABL_TR) || defined(KT_ABL_TW)
+                    tv[i] = 0u;
+#else
+                    tv[i] = T[e[i] & 0xFFFFu];
+#endif
+#ifndef KT_ABL_TW
+                    T[(e[i] & KS_LAST) ? (e[i] & 0xFFFFu) : LZF_SLOTS + lane] = (uint16_t)(B + 64u * i + lane);
+#endif
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < KT_WIN; i++)
+                    Ok[64u * i + lane] = (uint16_t)((e[i] & KS_PRED) ? B + 64u * i + ((e[i] >> KS_PL) & 63u) : tv[i]);
+            }
+        } else {
+            /* ---- C2(t-3): agreement and record; Q <- O of that block ------- */
+            if (t >= 3u && t - 3u < nb) {
+                const uint32_t k = t - 3u;
+                if (c_p < np) {
+                    uint32_t r = 0u;
+                    if (c_q1) {
+                        const uint64_t x1 = ((uint64_t)(c_a.y ^ c_b1.y) << 32) | (uint64_t)(c_a.x ^ c_b1.x);
+                        uint32_t k1 = x1 ? (uint32_t)__builtin_ctzll(x1) >> 3 : 8u;
+                        k1 = k1 < c_avail ? k1 : c_avail;
+                        r = (c_p - c_q1 - 1u) | (kt_code(k1) << 13);
+                        if (c_q2) {
+                            const uint64_t x2 = ((uint64_t)(c_a.y ^ c_b2.y) << 32) | (uint64_t)(c_a.x ^ c_b2.x);
+                            uint32_t k2 = x2 ? (uint32_t)__builtin_ctzll(x2) >> 3 : 8u;
+                            k2 = k2 < c_avail ? k2 : c_avail;
+                            r |= ((c_p - c_q2 - 1u) | (kt_code(k2) << 13)) << 16;
+                        }
+                    }
+                    rec[c_p] = r;
+                }
+                const uint32_t x = KT_BLK * k + 64u * j + lane;
+                if (x < np) Q[x & (LZF_WINDOW - 1u)] = O[KT_BLK * (k % 3u) + 64u * j + lane];
+            }
+            KT_TM(2);
+            /* ---- C1(t-2): q1, q2; their agreement loads below ---------------- */
+            c_p = 0xFFFFFFFFu;
+            c_q1 = c_q2 = 0u;
+            if (t >= 2u && t - 2u < nb) {
+                const uint32_t k = t - 2u, B = KT_BLK * k;
+                const uint32_t p = B + 64u * j + lane;
+                if (p < np) {
+                    c_p = p;
+                    const uint16_t *Ok = O + KT_BLK * (k % 3u), *Op = O + KT_BLK * ((k + 2u) % 3u);
+                    const uint32_t q1 = Ok[64u * j + lane];
+                    c_avail = n - p;
+                    c_a = ak[(PS + KT_PF - 2u) % KT_PF];              /* A's bytes of block t-2 */
+                    if (q1 != 0u && p - q1 <= LZF_WINDOW) {          /* off = p - q - 1 < 8192 */
+                        const uint32_t q2 = q1 >= B ? Ok[q1 - B]
+                                          : q1 + KT_BLK >= B ? Op[q1 + KT_BLK - B]
+                                                             : Q[q1 & (LZF_WINDOW - 1u)];
+                        c_q1 = l1 = q1;
+                        if (q2 != 0u && p - q2 <= LZF_WINDOW) c_q2 = l2 = q2;
+                    }
+                }
+            }
+            KT_TM(3);
+            /* ---- A(t): the worker's window of block t ----------------------- */
+            if (t < nb) {
+                const uint32_t p = KT_BLK * t + 64u * j + lane;
+                const bool act = p < np;
+                const uint2 a = pf[PS];
+                ak[PS] = a;
+                const uint32_t s = dv_slot(a.x);
+                const uint32_t i0 = s & 63u, i1 = 64u + ((s >> 6) & 63u), i2 = 128u + (s >> 12);
+#ifndef KT_ABL_A
+                if (act) {
+                    __hip_atomic_fetch_or(&Dw[i0], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_or(&Dw[i1], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_or(&Dw[i2], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                kt_wave_fence();
+#endif
+#ifdef KT_ABL_A
+                const unsigned long long M = act ? mine : 0ull;
+#else
+                const unsigned long long M = act ? (Dw[i0] & Dw[i1] & Dw[i2]) : 0ull;   /* same-slot lanes */
+                kt_wave_fence();
+                if (act) {
+                    Dw[i0] = 0ull;
+                    Dw[i1] = 0ull;
+                    Dw[i2] = 0ull;
+                }
+#endif
+                const unsigned long long pb = M & below;
+                const uint32_t pl = pb ? 63u - (uint32_t)__builtin_clzll(pb) : 0u;
+                S[KT_BLK * (t & 1u) + 64u * j + lane] =
+                    act ? (s | KS_ACT | (pb ? KS_PRED : 0u) | ((M >> lane) == 1ull ? KS_LAST : 0u) | (pl << KS_PL))
+                        : 0u;
+            }
+        }
+        if (w) KT_TM(4);
+        else KT_TM(0);
+        /* the step's loads: agreement bytes of C1 first, then the input of
+         * block t + KT_PF, so a wait for the former never waits for it */
+#ifdef KT_ABL_C
+        l1 = l2 = 0u;
+#endif
+        c_b1 = kt_ld8<SMALL>(src, n, l1);
+        c_b2 = kt_ld8<SMALL>(src, n, l2);
+        pf[PS] = kt_ld8<SMALL>(src, n, lp);
+        if (w) KT_TM(5);
+#ifndef KT_ABL_S
+        __syncthreads();
+#endif
+        if (w) KT_TM(6);
+        else KT_TM(1);
+#ifdef KT_TIMING
+        kt_acc[7]++;
+#endif
+    };
+    for (uint32_t t = 0; t < nb + 3u; t += KT_PF) {
+        step(KtIc<0>{}, t);
+        step(KtIc<1>{}, t + 1u);
+        step(KtIc<2>{}, t + 2u);
+        step(KtIc<3>{}, t + 3u);
+    }
+#ifdef KT_TIMING
+    if (lane == 0u)
+        for (uint32_t i = 0; i < 8u; i++) atomicAdd(&kt_times[i], (unsigned long long)kt_acc[i]);
+#endif
+}
+
+__global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt, LzfRecScratch sc)
+{
+    __shared__ __attribute__((aligned(16))) uint16_t T[LZF_SLOTS + 64u];  /* slot -> latest position, 0: none; + dummies */
+    __shared__ uint16_t Q[LZF_WINDOW];                                 /* q1 of position x at x % 8192 */
+    __shared__ uint32_t S[2u * KT_BLK];
+    __shared__ uint16_t O[3u * KT_BLK];                                /* q1 of the blocks' positions */
+    __shared__ unsigned long long D[KT_WIN][144];                      /* slot digit bitmaps per worker */
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const KtLds L{T, Q, O, S, D[w ? w - 1u : 0u]};
+#ifdef KT_PRIO
+    if (w == 0u) __builtin_amdgcn_s_setprio(KT_PRIO);   /* the table wave is the step's critical path */
+#endif
+    if (w)
+        for (uint32_t k = lane; k < 144u; k += 64u) D[w - 1u][k] = 0ull;
+    for (uint32_t v = blockIdx.x; v < bt.count; v += gridDim.x) {
+        const uint32_t n = bt.in_len[v];
+        if (n < 3u || n > LZF_SLOTS) continue;                  /* no positions (uniform per workgroup) */
+        const uint8_t *src = bt.in + bt.in_off[v];
+        uint32_t *rec = sc.rec + (uint64_t)v * sc.rstride;
+        if (n >= 8u) kt_value<false>(L, src, n, rec);
+        else kt_value<true>(L, src, n, rec);
+    }
+}
+
+/* ======================================================================== */
+/* kernel 2: the greedy parse and emission, one lane per value              */
+/* ======================================================================== */
+
+#define K3_THREADS 256u
+#define K3_CB      16u          /* records per parse block: 64 bytes of one line */
+#define K3_RW      32u          /* bitmap words kept in LDS per lane (power of two) */
+
+/* rel codes of the walk, relative to p: the record codes 0..7, plus
+ * 8 (the first 3 bytes agree, length unknown) and 9 (unknown) */
+__device__ __forceinline__ uint32_t k3_comb(uint32_t rel, uint32_t code)
+{
+    /* p~q agree in 3 bytes and q~r agree in 3 bytes => p~r agree in 3;
+     * exactly one of them => p~r differ in the first 3 bytes */
+    if (rel == 9u) return 9u;
+    const bool e1 = rel >= 2u, e2 = code >= 2u;
+    return (e1 && e2) ? 8u : (e1 != e2) ? RC_DIFF : 9u;
+}
+
+enum { K3_STEP = 0, K3_RESOLVE = 1, K3_DECIDE = 2, K3_EXTEND = 3, K3_EMIT = 4, K3_DONE = 5 };
+
+/* The lanes of a wave are at different points of their values, so the loop
+ * is a state machine in which every lane does at most ONE unit of each kind
+ * of work per iteration -- take the record of p, test one candidate for
+ * insertion (or load one record of the chain), compare one 16-byte piece of
+ * a long match, emit one literal or one back-reference.  Every wave memory
+ * instruction touches one line per lane (64 values), so the kernel is shaped
+ * to issue few of them: records in 64-byte blocks, output in 16-byte stores,
+ * the input in 16-byte windows, the bitmap's recent words in LDS. */
+__global__ __launch_bounds__(K3_THREADS) void lzf_parse_rec_kernel(LzfBatch bt, LzfRecScratch sc)
+{
+    const uint32_t v = blockIdx.x * K3_THREADS + threadIdx.x;
+    if (v >= bt.count) return;
+    const uint32_t n = bt.in_len[v], cap = bt.out_cap[v];
+    if (n == 0u || cap == 0u || n > LZF_SLOTS) {                   /* src/lzf_c.c:131 */
+        bt.out_len[v] = 0u;
+        return;
+    }
+    const uint8_t *src = bt.in + bt.in_off[v];
+    uint8_t *dst = bt.out + bt.out_off[v];
+    const uint32_t *rec = sc.rec + (uint64_t)v * sc.rstride;
+    uint32_t *bits = sc.bits + (uint64_t)v * sc.bstride;
+
+    /* output: aligned dwords at da; acc holds the bytes from dword fw on;
+     * completed dwords [fs, fw) wait in pb0..2 and leave as one 16-byte store */
+    const uint32_t dm = (uint32_t)((uintptr_t)dst & 3u);
+    uint8_t *const da = dst - dm;
+    uint64_t acc = 0;
+    uint32_t accn = dm, fw = 0;
+    uint32_t hx = dm;                   /* header byte of the open run (index from da) */
+    uint32_t pb0 = 0u, pb1 = 0u, pb2 = 0u, fs = 0u;
+    /* input: the 16 bytes from position wb */
+    uint32_t wb = 0xFFFFFFF0u;
+    uint4 W = make_uint4(0, 0, 0, 0);
+
+    uint32_t o = 1u, run = 0u, p = 0u; /* o, run: the reference's op and lit (src/lzf_c.c:113-143) */
+    uint32_t cb = 0xFFFFFFF0u;         /* records [cb, cb + 16) in C0..C3 */
+    uint4 C0 = W, C1 = W, C2 = W, C3 = W;
+    uint32_t cw = 0u, curw = 0u;       /* inserted-bitmap word of p, in flight */
+    __shared__ uint32_t k3_ring[K3_RW][K3_THREADS];
+    uint32_t *const ring = &k3_ring[0][threadIdx.x];
+#define K3_RING(w_) ring[((w_) & (K3_RW - 1u)) * K3_THREADS]
+    uint32_t fl = 0u;                  /* bitmap words [0, fl) are in scratch */
+#define K3_FLUSH_TO(w_)                                                            \
+    do {                                                                           \
+        while (fl + K3_RW <= (w_)) {                                               \
+            *(uint4 *)(bits + fl) = make_uint4(K3_RING(fl), K3_RING(fl + 1u),      \
+                                               K3_RING(fl + 2u), K3_RING(fl + 3u)); \
+            fl += 4u;                                                              \
+        }                                                                          \
+    } while (0)
+    uint32_t ms = 0u, me = 0u;         /* the last match: [ms, me) */
+    uint32_t rel = 0u, q = 0u, k = 0u, lim = 0u, m = 0u;
+    uint32_t reln = 0u, qn = 0u;       /* the next chain link from the same record (reln 0: none) */
+    bool ok = true;
+    uint32_t mode = n >= 3u ? K3_STEP : K3_DONE;
+
+#define K3_PUT(bytes_, cnt_)                                                       \
+    do {                                                                           \
+        acc |= (uint64_t)(bytes_) << (8u * accn);                                  \
+        accn += (cnt_);                                                            \
+        if (accn >= 4u) {                                                          \
+            const uint32_t w_ = (uint32_t)acc;                                     \
+            if (fw == 0u && dm != 0u) {        /* the partial first dword */       \
+                for (uint32_t t_ = dm; t_ < 4u; t_++) da[t_] = (uint8_t)(w_ >> (8u * t_)); \
+                fs = 1u;                                                           \
+            } else {                                                               \
+                const uint32_t np_ = fw - fs;                                      \
+                if (np_ == 3u) {                                                   \
+                    const uint4 v_ = make_uint4(pb0, pb1, pb2, w_);                \
+                    __builtin_memcpy(da + 4u * fs, &v_, 16);                       \
+                    fs = fw + 1u;                                                  \
+                } else if (np_ == 0u) {                                            \
+                    pb0 = w_;                                                      \
+                } else if (np_ == 1u) {                                            \
+                    pb1 = w_;                                                      \
+                } else {                                                           \
+                    pb2 = w_;                                                      \
+                }                                                                  \
+            }                                                                      \
+            fw++;                                                                  \
+            acc >>= 32;                                                            \
+            accn -= 4u;                                                            \
+        }                                                                          \
+    } while (0)
+#define K3_PATCH(x_, byte_)                                                        \
+    do {                                                                           \
+        if ((x_) >= 4u * fw) {                                                     \
+            const uint32_t sh_ = 8u * ((x_) - 4u * fw);                            \
+            acc = (acc & ~(0xFFull << sh_)) | ((uint64_t)(byte_) << sh_);          \
+        } else if ((x_) >= 4u * fs) {                                              \
+            const uint32_t i_ = ((x_) >> 2) - fs, sh_ = 8u * ((x_) & 3u);          \
+            const uint32_t mk_ = ~(0xFFu << sh_), b_ = (uint32_t)(byte_) << sh_;  \
+            if (i_ == 0u) pb0 = (pb0 & mk_) | b_;                                  \
+            else if (i_ == 1u) pb1 = (pb1 & mk_) | b_;                             \
+            else pb2 = (pb2 & mk_) | b_;                                           \
+        } else {                                                                   \
+            da[(x_)] = (uint8_t)(byte_);                                           \
+        }                                                                          \
+    } while (0)
+#define K3_BYTE(pos_, out_)                                                        \
+    do {                                                                           \
+        uint32_t d_ = (pos_) - wb;                                                 \
+        if (d_ >= 16u) {                                                           \
+            W = dv_ld16_safe(src + (pos_), n - (pos_));                            \
+            wb = (pos_);                                                           \
+            d_ = 0u;                                                               \
+        }                                                                          \
+        (out_) = (dv_sel4(W, d_ >> 2) >> (8u * (d_ & 3u))) & 0xFFu;               \
+    } while (0)
+#define K3_LITERAL(pos_)                                                           \
+    do {                                                                           \
+        uint32_t byte_;                                                            \
+        K3_BYTE(pos_, byte_);                                                      \
+        if (run == 0u) { hx = 4u * fw + accn; K3_PUT(byte_ << 8, 2u); }           \
+        else K3_PUT(byte_, 1u);                                                    \
+        o++;                                                                       \
+        if (++run == LZF_MAX_LIT) { K3_PATCH(hx, LZF_MAX_LIT - 1u); run = 0u; o++; } \
+    } while (0)
+
+    while (__ballot(mode != K3_DONE)) {
+        /* ---- the record of p ---------------------------------------------- */
+        if (mode == K3_STEP) {                                            /* src/lzf_c.c:145 */
+            if (p >= n - 2u) {
+                mode = K3_DONE;
+            } else {
+                uint32_t d = p - cb;
+                if (d >= K3_CB) {
+                    cb = p & ~(K3_CB - 1u);
+                    d = p - cb;
+                    const uint4 *cp = (const uint4 *)(rec + cb);
+                    C0 = cp[0];
+                    C1 = cp[1];
+                    C2 = cp[2];
+                    C3 = cp[3];
+                }
+                /* a select tree over the 16 words (a dynamic index would put
+                 * the block in scratch memory) */
+                const bool b0 = d & 1u, b1 = d & 2u;
+                const uint32_t c0 = b1 ? (b0 ? C0.w : C0.z) : (b0 ? C0.y : C0.x);
+                const uint32_t c1 = b1 ? (b0 ? C1.w : C1.z) : (b0 ? C1.y : C1.x);
+                const uint32_t c2 = b1 ? (b0 ? C2.w : C2.z) : (b0 ? C2.y : C2.x);
+                const uint32_t c3 = b1 ? (b0 ? C3.w : C3.z) : (b0 ? C3.y : C3.x);
+                const uint32_t c = (d & 8u) ? ((d & 4u) ? c3 : c2) : ((d & 4u) ? c1 : c0);
+                rel = (c >> 13) & 7u;
+                q = p - 1u - (c & 0x1FFFu);
+                reln = c >> 29;
+                qn = p - 1u - ((c >> 16) & 0x1FFFu);
+                mode = rel ? K3_RESOLVE : K3_DECIDE;
+            }
+        }
+        /* ---- is the candidate inserted? else the next chain link ---------- */
+        if (mode == K3_RESOLVE) {
+            uint32_t word;
+            if (q >= ms) {
+                word = (q > ms && q + 3u <= me) ? 0u : 0xFFFFFFFFu;         /* last match's interior */
+            } else {
+                const uint32_t d = cw - (q >> 5);
+                word = d == 0u ? curw : (q >> 5) >= fl ? K3_RING(q >> 5) : bits[q >> 5];
+            }
+            if ((word >> (q & 31u)) & 1u) {                              /* q is the ref */
+                if (rel == 9u)
+                    rel = (src[q] == src[p] && src[q + 1u] == src[p + 1u] && src[q + 2u] == src[p + 2u]) ? 8u
+                                                                                                        : RC_DIFF;
+                mode = K3_DECIDE;
+            } else if (reln) {                                           /* the record's second link */
+                q = qn;
+                rel = reln;
+                reln = 0u;
+                /* the link after it needs q's own record: mark with reln 0 and
+                 * qn = q (a load below on the next failure) */
+                qn = 0xFFFFFFFFu;
+            } else if (qn == 0xFFFFFFFFu) {                              /* load q's record: two more links */
+                const uint32_t c2 = rec[q];
+                const uint32_t r1 = (c2 >> 13) & 7u, r2 = c2 >> 29;
+                const uint32_t y1 = q - 1u - (c2 & 0x1FFFu), y2 = q - 1u - ((c2 >> 16) & 0x1FFFu);
+                if (!r1 || p - y1 - 1u >= LZF_WINDOW) {                  /* the chain leaves p's window */
+                    rel = 0u;
+                    mode = K3_DECIDE;
+                } else {
+                    const uint32_t rq = rel;
+                    rel = k3_comb(rq, r1);
+                    q = y1;
+                    if (r2 && p - y2 - 1u < LZF_WINDOW) {
+                        reln = k3_comb(rq, r2);
+                        qn = y2;
+                    } else {
+                        reln = 0u;
+                        qn = 0u;                                         /* nothing after y1 */
+                    }
+                }
+            } else {                                                     /* no further link */
+                rel = 0u;
+                mode = K3_DECIDE;
+            }
+        }
+        /* ---- literal, or the start of a back-reference --------------------- */
+        if (mode == K3_DECIDE) {
+            curw |= 1u << (p & 31u);                                     /* p is inserted */
+            if (!(rel >= 2u && p + 4u < n)) {                            /* src/lzf_c.c:151-166 */
+                if (o >= cap) {                                          /* src/lzf_c.c:263 */
+                    ok = false;
+                    mode = K3_DONE;
+                } else {
+                    K3_LITERAL(p);
+                    p++;
+                    if ((p & 31u) == 0u) {
+                        K3_FLUSH_TO(cw);
+                        K3_RING(cw) = curw;
+                        cw++;
+                        curw = 0u;
+                    }
+                    mode = K3_STEP;
+                }
+            } else {
+                uint32_t maxlen = n - p - 2u;                            /* src/lzf_c.c:169-170 */
+                if (maxlen > LZF_MAX_REF) maxlen = LZF_MAX_REF;
+                /* the 16 unrolled compares run whenever maxlen > 16 (src/lzf_c.c:181-202) */
+                lim = (maxlen > 16u && maxlen < 19u) ? 19u : maxlen;
+                if (rel <= 6u) {
+                    m = rel + 1u < lim ? rel + 1u : lim;
+                    mode = K3_EMIT;
+                } else {
+                    k = rel == RC_LONG ? 8u : 3u;
+                    mode = K3_EXTEND;
+                }
+            }
+        }
+        /* ---- one 16-byte piece of a long match ----------------------------- */
+        if (mode == K3_EXTEND) {
+            if (k < lim) {
+                const uint32_t avail = n - (p + k);
+                const uint4 a = dv_ld16_safe(src + p + k, avail), b = dv_ld16_safe(src + q + k, avail);
+                W = a;                                   /* literals after the match read it */
+                wb = p + k;
+                const uint32_t d = dv_first_diff(a, b);
+                k += d;
+                if (d < 16u) lim = k < lim ? k : lim;
+            }
+            if (k >= lim) {
+                m = lim;
+                mode = K3_EMIT;
+            }
+        }
+        /* ---- the back-reference -------------------------------------------- */
+        if (mode == K3_EMIT) {
+            const uint32_t off = p - q - 1u;
+            if (run) K3_PATCH(hx, run - 1u);                             /* close the run */
+            else o--;                                                    /* undo empty run */
+            if (o + 4u >= cap) {                                         /* src/lzf_c.c:176 */
+                ok = false;
+                mode = K3_DONE;
+            } else {
+                const uint32_t L = m - 2u;
+                if (L < 7u) {
+                    K3_PUT(((off >> 8) | (L << 5)) | ((off & 0xFFu) << 8), 2u);
+                    o += 2u;
+                } else {
+                    K3_PUT((0xE0u | (off >> 8)) | ((L - 7u) << 8) | ((off & 0xFFu) << 16), 3u);
+                    o += 3u;
+                }
+                run = 0u;
+                o++;                                                     /* reserve a header */
+                ms = p;
+                p += m;
+                me = p;
+                if (p >= n - 2u) {                                       /* src/lzf_c.c:229 */
+                    mode = K3_DONE;
+                } else {
+                    /* the two last positions of the match are inserted, its interior not */
+                    const uint32_t nw = p >> 5, t1 = p - 2u, t2 = p - 1u;
+                    const uint32_t b1 = 1u << (t1 & 31u), b2 = 1u << (t2 & 31u);
+                    if (nw == cw) {
+                        curw |= b1 | b2;
+                    } else {
+                        uint32_t wo = curw, wm = 0u, wn = 0u;
+                        if ((t1 >> 5) == cw) wo |= b1; else if ((t1 >> 5) == nw) wn |= b1; else wm |= b1;
+                        if ((t2 >> 5) == cw) wo |= b2; else if ((t2 >> 5) == nw) wn |= b2; else wm |= b2;
+                        K3_FLUSH_TO(cw);
+                        K3_RING(cw) = wo;
+                        /* words cw+1 .. nw-2 are all interior (0), nw-1 holds tails */
+                        for (uint32_t w = cw + 1u; w < nw; w++) {
+                            K3_FLUSH_TO(w);
+                            K3_RING(w) = w + 1u == nw ? wm : 0u;
+                        }
+                        curw = wn;
+                        cw = nw;
+                    }
+                    mode = K3_STEP;
+                }
+            }
+        }
+    }
+    if (!ok || o + 3u > cap) { bt.out_len[v] = 0u; return; }          /* src/lzf_c.c:276 */
+    while (p < n) {                                                   /* src/lzf_c.c:279-288 */
+        K3_LITERAL(p);
+        p++;
+    }
+    if (run) K3_PATCH(hx, run - 1u);
+    else o--;
+    for (uint32_t i = fs; i < fw; i++)
+        *(uint32_t *)(da + 4u * i) = i == fs ? pb0 : i == fs + 1u ? pb1 : pb2;
+    for (uint32_t t = 0; t < accn; t++)
+        if (4u * fw + t >= dm) da[4u * fw + t] = (uint8_t)(acc >> (8u * t));
+    bt.out_len[v] = o;
+#undef K3_PUT
+#undef K3_PATCH
+#undef K3_BYTE
+#undef K3_LITERAL
+#undef K3_RING
+#undef K3_FLUSH_TO
+}
+
+/* ---- launcher ------------------------------------------------------------ */
+
+/* records per value: a multiple of 16 (64 bytes) plus one block of slack, so
+ * the parse's 64-byte blocks never straddle a line and never leave the value */
+static uint64_t rec_stride(uint32_t max_len) { return (((uint64_t)max_len + 15u) & ~15ull) + 16u; }
+static uint64_t rec_bstride(uint32_t max_len) { return ((((uint64_t)max_len + 31u) >> 5) + 3u) & ~3ull; }
+
+size_t lzf_table_scratch_per_value(uint32_t max_len)
+{
+    return (size_t)(rec_stride(max_len) * 4u + rec_bstride(max_len) * 4u);
+}
+
+bool lzf_table_compress_supported(uint32_t max_len) { return max_len <= LZF_SLOTS; }
+
+hipError_t lzf_launch_compress_table(const LzfBatch &b, hipStream_t s, void *scratch, size_t scratch_bytes)
+{
+    if (b.max_len > LZF_SLOTS) return hipErrorInvalidValue;
+    const uint64_t rstride = rec_stride(b.max_len), bstride = rec_bstride(b.max_len);
+    const size_t per = lzf_table_scratch_per_value(b.max_len);
+    const auto bytes_for = [&](uint64_t ch) { return ((ch * rstride * 4u + 255u) & ~255ull) + ch * bstride * 4u; };
+    uint64_t chunk = scratch_bytes / per;
+    if (chunk > b.count) chunk = b.count;
+    while (chunk && bytes_for(chunk) > scratch_bytes) chunk--;
+    if (chunk == 0) return hipErrorInvalidValue;
+    /* diagnostics: LZF_GPU_TABLE_STAGE=1 runs kernel 1 only (its own time) */
+    const char *stg = getenv("LZF_GPU_TABLE_STAGE");
+    const bool cand_only = stg && *stg == '1';
+    LzfRecScratch sc;
+    sc.rec = (uint32_t *)scratch;
+    sc.bits = (uint32_t *)((uint8_t *)scratch + ((chunk * rstride * 4u + 255u) & ~255ull));
+    sc.rstride = rstride;
+    sc.bstride = bstride;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    hipError_t e;
+    for (uint64_t first = 0; first < b.count; first += chunk) {
+        const uint32_t cnt = (uint32_t)((b.count - first) < chunk ? (b.count - first) : chunk);
+        LzfBatch c = b;
+        c.in_off = b.in_off + first;
+        c.in_len = b.in_len + first;
+        c.out_off = b.out_off + first;
+        c.out_cap = b.out_cap + first;
+        c.out_len = b.out_len + first;
+        c.count = cnt;
+        /* one 512-thread workgroup per CU (the table is 128 KiB), persistent */
+        const uint32_t g = cnt < (uint32_t)cus ? cnt : (uint32_t)cus;
+        hipLaunchKernelGGL(lzf_cand_table_kernel, dim3(g), dim3(KT_THREADS), 0, s, c, sc);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (cand_only) continue;
+        hipLaunchKernelGGL(lzf_parse_rec_kernel, dim3((cnt + K3_THREADS - 1u) / K3_THREADS), dim3(K3_THREADS),
+                           0, s, c, sc);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}

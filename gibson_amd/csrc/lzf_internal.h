@@ -63,7 +63,19 @@ struct LzfLaneScratch {
     uint32_t force_fix;    /* diagnostics: take the atomic-order repair path */
 };
 
+/* compress scratch of the table generation (lzf_cand.hip), device pointers:
+ * per value rstride u32 records and bstride u32 inserted-bitmap words */
+struct LzfRecScratch {
+    uint32_t *rec;
+    uint32_t *bits;
+    uint64_t rstride;
+    uint64_t bstride;
+};
+
 /* launchers, defined next to their kernels; return hipSuccess or the error */
+hipError_t lzf_launch_compress_table(const LzfBatch &b, hipStream_t s, void *scratch, size_t scratch_bytes);
+size_t lzf_table_scratch_per_value(uint32_t max_len);
+bool lzf_table_compress_supported(uint32_t max_len);
 hipError_t lzf_launch_decompress_lane(const LzfBatch &b, hipStream_t s);
 /* aux / ev (4 events) optional: chunks pipelined over s (kernel 1) and aux
  * (kernel 2); s is joined with aux before returning */

@@ -17,7 +17,7 @@ from tests.oracle_lib import sha16, synth
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-GENERATIONS = ["lane", "window", "serial"]
+GENERATIONS = ["table", "lane", "window", "serial"]
 
 
 @pytest.fixture(autouse=True)
@@ -30,7 +30,7 @@ def _lane_for_any_batch(monkeypatch):
 
 @pytest.fixture(params=GENERATIONS)
 def generation(request, monkeypatch):
-    if request.param == "lane":
+    if request.param == "table":
         monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
     else:
         monkeypatch.setenv("LZF_GPU_KERNEL", request.param)
@@ -131,7 +131,7 @@ def test_batch_decompress_other_generations(golden, oracle, monkeypatch, gen):
 
 def test_lane_decoder_edge_and_unaligned(oracle, monkeypatch):
     from tests.gpu_batch import gpu_decompress
-    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.setenv("LZF_GPU_KERNEL", "lane")
     monkeypatch.setenv("LZF_GPU_DECOMPRESS", "lane")
     streams = [b"", b"\x00", b"\xe0\x00\x00", b"\x1f" + b"q" * 31, b"\x00z\xa0\x00"]
     for cap in (0, 1, 7, 8, 32, 4096):
@@ -167,7 +167,7 @@ def test_unaligned_arenas(oracle, generation, align):
 def test_lane_mid_class(oracle, monkeypatch):
     # the mid-class lane kernels (values 4 KiB .. 64 KiB), opt-in
     from tests.gpu_batch import gpu_compress
-    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.setenv("LZF_GPU_KERNEL", "lane")
     monkeypatch.setenv("LZF_GPU_LANE_MID", "1")
     monkeypatch.setenv("LZF_GPU_LANE_RING", "0")
     rnd = random.Random(21)
@@ -182,7 +182,7 @@ def test_lane_ring_class(oracle, monkeypatch, align):
     # last 8 KiB of positions, window tests on heads and links, and past
     # 16 KiB the bytes streamed through an LDS ring
     from tests.gpu_batch import gpu_compress, gpu_decompress
-    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.setenv("LZF_GPU_KERNEL", "lane")
     monkeypatch.setenv("LZF_GPU_LANE_RING", "1")
     rnd = random.Random(33 + align)
     vals = []
@@ -208,10 +208,28 @@ def test_lane_scratch_chunks(oracle, monkeypatch, nmax):
     # the scratch is per host thread, so a fresh thread sees the cap
     import threading
     from tests.gpu_batch import gpu_compress
-    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.setenv("LZF_GPU_KERNEL", "lane")
     monkeypatch.setenv("LZF_GPU_SCRATCH_MB", "4")
     rnd = random.Random(nmax)
     vals = [synth(rnd.randrange(6), 0x5EED00FA, i, rnd.randint(1, nmax)) for i in range(400)]
+    caps = [max(1, len(v) - 4) for v in vals]
+    out = {}
+    th = threading.Thread(target=lambda: out.setdefault("r", gpu_compress(vals, caps, align=3)))
+    th.start()
+    th.join()
+    assert out["r"] == [oracle.compress(v, c) for v, c in zip(vals, caps)]
+
+
+@pytest.mark.parametrize("nmax", [4096, 65536])
+def test_table_scratch_chunks(oracle, monkeypatch, nmax):
+    # the table generation over many scratch chunks (4 MiB cap on a fresh
+    # host thread: the scratch is per host thread)
+    import threading
+    from tests.gpu_batch import gpu_compress
+    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.setenv("LZF_GPU_SCRATCH_MB", "4")
+    rnd = random.Random(nmax + 1)
+    vals = [synth(rnd.randrange(6), 0x5EED00FB, i, rnd.randint(1, nmax)) for i in range(300)]
     caps = [max(1, len(v) - 4) for v in vals]
     out = {}
     th = threading.Thread(target=lambda: out.setdefault("r", gpu_compress(vals, caps, align=3)))
@@ -225,7 +243,7 @@ def test_wave_parse(oracle, monkeypatch, align):
     # the wave form of the parse kernel (64 positions per step, opt-in):
     # every size class edge of a window, caps that run out inside a window
     from tests.gpu_batch import gpu_compress
-    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.setenv("LZF_GPU_KERNEL", "lane")
     monkeypatch.setenv("LZF_GPU_LANE_PARSE", "wave")
     rnd = random.Random(77 + align)
     vals = [synth(rnd.randrange(6), 0x5EED00E0, i, rnd.randint(1, 4096)) for i in range(400)]
@@ -251,7 +269,7 @@ def test_lane_order_repair_path(oracle, monkeypatch):
     # serialise a wave's same-address atomics in lane order) gives the same
     # streams
     from tests.gpu_batch import gpu_compress
-    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.setenv("LZF_GPU_KERNEL", "lane")
     monkeypatch.setenv("LZF_GPU_LANE_FORCE_FIX", "1")
     monkeypatch.setenv("LZF_GPU_LANE_MID", "1")
     monkeypatch.setenv("LZF_GPU_LANE_RING", "0")
