@@ -181,10 +181,14 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
         /* batches with values past 64 KiB, and small batches, go to the window
          * generation: the parse runs one value per lane, so its time has a
          * floor of one whole value's parse (~5 ms); below the crossover one
-         * wave per value finishes first (tools/crossover.py) */
-        return (lzf_table_compress_supported(b.max_len) && b.count >= lane_min_count(b.max_len))
-                   ? lane_compress(b, s, true)
-                   : lzf_launch_compress(b, s);
+         * wave per value finishes first (tools/crossover.py).  Values of at
+         * most 4 KiB take the lane generation's small class (json4k: 56.7 vs
+         * 79.6 ms for the table's per-value 128 KiB table); past 4 KiB the
+         * table generation (text8k 145 vs 162 ms, mixed16k 329 vs 541 ms,
+         * text64k 262 vs 485 ms; profiles/r02/workloads.txt) */
+        if (b.count < lane_min_count(b.max_len) || !lzf_table_compress_supported(b.max_len))
+            return lzf_launch_compress(b, s);
+        return lane_compress(b, s, b.max_len > 4096u);
     }
 }
 
@@ -652,7 +656,7 @@ const char *lzf_gpu_kernel_info(void)
             (lane_decoder() ? "lane" : lzf_decompress_kernel_name());
         break;
     default:
-        s = std::string("compress=table(cand_table+parse_rec; window64 past 64 KiB or below ") +
+        s = std::string("compress=table(cand_table+parse_rec; lane small class up to 4 KiB; window64 past 64 KiB or below ") +
             std::to_string(lane_min_count(4096u)) + " values of <= 4 KiB / " +
             std::to_string(lane_min_count(8192u)) + " of <= 8 KiB / " +
             std::to_string(lane_min_count(16384u)) + " of <= 16 KiB / " +

@@ -50,7 +50,14 @@
 #define RC_DIFF 1u
 #define RC_LONG 7u
 
-#define KT_WIN 7u                 /* windows of 64 positions per block = worker waves */
+#ifndef KT_WIN
+#define KT_WIN 14u                /* windows of 64 positions per block = worker waves */
+#endif
+/* same-slot lanes of a window: from three LDS digit bitmaps per worker
+ * (KT_BALLOT 0) or from 16 ballots of the slot's bits (1; no LDS) */
+#ifndef KT_BALLOT
+#define KT_BALLOT (KT_WIN > 7u)
+#endif
 #define KT_BLK (64u * KT_WIN)
 #define KT_THREADS (64u * (KT_WIN + 1u))
 #ifndef KT_PF
@@ -259,18 +266,23 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 const uint2 a = pf[PS];
                 ak[PS] = a;
                 const uint32_t s = dv_slot(a.x);
+#if KT_BALLOT
+                /* exact: the lanes agreeing with mine on every slot bit */
+                unsigned long long M = __ballot(act);
+#pragma unroll
+                for (uint32_t b = 0; b < 16u; b++) {
+                    const unsigned long long bb = __ballot((s >> b) & 1u);
+                    M &= ((s >> b) & 1u) ? bb : ~bb;
+                }
+                if (!act) M = 0ull;
+#else
                 const uint32_t i0 = s & 63u, i1 = 64u + ((s >> 6) & 63u), i2 = 128u + (s >> 12);
-#ifndef KT_ABL_A
                 if (act) {
                     __hip_atomic_fetch_or(&Dw[i0], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     __hip_atomic_fetch_or(&Dw[i1], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     __hip_atomic_fetch_or(&Dw[i2], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 kt_wave_fence();
-#endif
-#ifdef KT_ABL_A
-                const unsigned long long M = act ? mine : 0ull;
-#else
                 const unsigned long long M = act ? (Dw[i0] & Dw[i1] & Dw[i2]) : 0ull;   /* same-slot lanes */
                 kt_wave_fence();
                 if (act) {
@@ -324,14 +336,23 @@ __global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt,
     __shared__ uint16_t Q[LZF_WINDOW];                                 /* q1 of position x at x % 8192 */
     __shared__ uint32_t S[2u * KT_BLK];
     __shared__ uint16_t O[3u * KT_BLK];                                /* q1 of the blocks' positions */
+#if KT_BALLOT
+    unsigned long long *const Dw = nullptr;
+#else
     __shared__ unsigned long long D[KT_WIN][144];                      /* slot digit bitmaps per worker */
+#endif
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const KtLds L{T, Q, O, S, D[w ? w - 1u : 0u]};
+#if !KT_BALLOT
+    unsigned long long *const Dw = D[w ? w - 1u : 0u];
+#endif
+    const KtLds L{T, Q, O, S, Dw};
 #ifdef KT_PRIO
     if (w == 0u) __builtin_amdgcn_s_setprio(KT_PRIO);   /* the table wave is the step's critical path */
 #endif
+#if !KT_BALLOT
     if (w)
-        for (uint32_t k = lane; k < 144u; k += 64u) D[w - 1u][k] = 0ull;
+        for (uint32_t k = lane; k < 144u; k += 64u) Dw[k] = 0ull;
+#endif
     for (uint32_t v = blockIdx.x; v < bt.count; v += gridDim.x) {
         const uint32_t n = bt.in_len[v];
         if (n < 3u || n > LZF_SLOTS) continue;                  /* no positions (uniform per workgroup) */
