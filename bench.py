@@ -101,11 +101,22 @@ def launch_ranks(a):
 
 
 def cpu_cores():
-    """Cores this process may run on (the affinity set, i.e. nproc)."""
+    """(cores, note): the CPUs this process may run on -- its affinity set,
+    capped by the cgroup CPU quota (cpu.max) where one is set: on the GPU box
+    the affinity lists the whole machine (256) while the quota grants 16."""
     try:
-        return len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        return os.cpu_count() or 1
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    cores = min(aff, quota) if quota else aff
+    return cores, f"affinity {aff} CPUs, cgroup quota {quota if quota else 'none'}"
 
 
 def _cpu_run(kind, seed, n, count, threads, reps):
@@ -314,9 +325,12 @@ def main():
             },
         }
         if world == 1 and not a.no_cpu:
-            threads = a.cpu_threads or cpu_cores()
+            cores, note = cpu_cores()
+            threads = a.cpu_threads or cores
             cnt = a.cpu_count or min(count, max(4 * threads, (4 << 30) // n))
             line["cpu_baseline"] = cpu_baseline(kind, seed, n, cnt, threads)
+            if line["cpu_baseline"] and "error" not in line["cpu_baseline"]:
+                line["cpu_baseline"]["cores_note"] = note
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -435,9 +449,12 @@ def main_decompress(a, world, rank, dev, cfg_idx, kind, seed, n, count):
             },
         }
         if world == 1 and not a.no_cpu:
-            threads = a.cpu_threads or cpu_cores()
+            cores, note = cpu_cores()
+            threads = a.cpu_threads or cores
             cnt = a.cpu_count or min(count, max(4 * threads, (4 << 30) // n))
             line["cpu_baseline"] = cpu_baseline(kind, seed, n, cnt, threads, decode_only=True)
+            if line["cpu_baseline"] and "error" not in line["cpu_baseline"]:
+                line["cpu_baseline"]["cores_note"] = note
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -18,6 +18,7 @@ from .lzf import (  # noqa: F401
     compress_batch,
     decompress_batch,
     kernel_info,
+    release,
     lib,
     lib_path,
     lzf_compress,

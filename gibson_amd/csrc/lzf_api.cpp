@@ -28,8 +28,10 @@
 #include "../../include/lzf.h"
 #include "../../include/lzf_gpu.h"
 
+#ifdef LZF_DIAG
 hipError_t lzf_launch_compress_serial(const LzfBatch &b, hipStream_t s);
 hipError_t lzf_launch_decompress_serial(const LzfBatch &b, hipStream_t s);
+#endif
 
 namespace {
 
@@ -43,7 +45,9 @@ enum KernelGen { GEN_TABLE = 0, GEN_LANE = 1, GEN_WINDOW = 2, GEN_SERIAL = 3 };
 KernelGen kernel_gen()
 {
     const char *e = getenv("LZF_GPU_KERNEL");
+#ifdef LZF_DIAG
     if (e && !strcmp(e, "serial")) return GEN_SERIAL;
+#endif
     if (e && !strcmp(e, "window")) return GEN_WINDOW;
     if (e && !strcmp(e, "lane")) return GEN_LANE;
     return GEN_TABLE;
@@ -70,19 +74,26 @@ int current_device_ok()
     return device_ok(dev) ? LZF_GPU_OK : LZF_GPU_ENODEV;
 }
 
-/* Compress scratch of the lane generation (cand words + inserted bitmap),
- * one per (host thread, device), grown on demand up to LZF_GPU_SCRATCH_MB
- * (default 40 GiB: 1 M values of 8 KiB or 256 K of 64 KiB in one chunk; larger batches run in chunks).  A batch on another stream
- * than the previous user waits for that user's kernels first. */
+/* Compress scratch (records/cand words + inserted bitmap), ONE per device,
+ * shared by every host thread under a mutex and grown on demand (cap:
+ * scratch_limit).  The mutex is held while a batch is enqueued; a batch on
+ * another stream than the previous user first waits for that user's
+ * kernels (an event), so concurrent callers stay correct.  lzf_gpu_release()
+ * frees it. */
 struct Scratch {
+    std::mutex mu;
     void *p = nullptr;
     size_t cap = 0;
     hipEvent_t ev = nullptr;
     hipStream_t last = nullptr;
     bool used = false;
+#ifdef LZF_DIAG
     hipStream_t aux = nullptr;      /* kernel-2 stream of the chunk pipeline */
     hipEvent_t pev[4] = {nullptr, nullptr, nullptr, nullptr};
+#endif
 };
+
+Scratch g_scratch[64];
 
 /* Scratch cap: LZF_GPU_SCRATCH_MB if set, else half of the device memory
  * free when the scratch grows (at least 1 GiB): a whole BASELINE batch
@@ -102,51 +113,65 @@ size_t scratch_limit(size_t held)
     return lim > ((size_t)1 << 30) ? lim : ((size_t)1 << 30);
 }
 
+void scratch_free(Scratch &S)
+{
+    if (S.p) {
+        if (S.used && S.ev) (void)hipEventSynchronize(S.ev);
+        (void)hipFree(S.p);
+    }
+    S.p = nullptr;
+    S.cap = 0;
+    S.used = false;
+}
+
 hipError_t lane_compress(const LzfBatch &b, hipStream_t s, bool table)
 {
-    static thread_local Scratch per_dev[64];
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    Scratch &S = per_dev[dev & 63];
+    Scratch &S = g_scratch[dev & 63];
+    std::lock_guard<std::mutex> lk(S.mu);
     const size_t per = table ? lzf_table_scratch_per_value(b.max_len) : lzf_lane_scratch_per_value(b.max_len);
     size_t want = per * (size_t)b.count + 512;
     const size_t lim = scratch_limit(S.cap);
     if (want > lim) want = lim;
     if (want < 2 * per + 1024) want = 2 * per + 1024;     /* two pipeline halves */
     if (S.cap < want) {
-        if (S.p) {
-            (void)hipDeviceSynchronize();
-            (void)hipFree(S.p);
-            S.p = nullptr;
-            S.cap = 0;
-        }
+        scratch_free(S);
         /* short of device memory: a smaller scratch only means more chunks */
         const size_t least = 2 * per + 1024;
         while ((e = hipMalloc(&S.p, want)) != hipSuccess && want > least) {
             (void)hipGetLastError();
             want = want / 2 > least ? want / 2 : least;
         }
-        if (e != hipSuccess) return e;
+        if (e != hipSuccess) {
+            S.p = nullptr;
+            return e;
+        }
         S.cap = want;
-        S.used = false;
     }
     if (!S.ev && (e = hipEventCreateWithFlags(&S.ev, hipEventDisableTiming)) != hipSuccess) return e;
     if (S.used && S.last != s && (e = hipStreamWaitEvent(s, S.ev, 0)) != hipSuccess) return e;
-    const char *ff = getenv("LZF_GPU_LANE_FORCE_FIX");
-    /* LZF_GPU_LANE_PIPE=1 overlaps the two kernels of consecutive chunks on
-     * two streams; off by default: both kernels hold LDS and do not co-reside
-     * well */
-    const char *pp = getenv("LZF_GPU_LANE_PIPE");
-    const bool pipe = pp && *pp == '1';
-    if (pipe && !S.aux) {
-        if ((e = hipStreamCreateWithFlags(&S.aux, hipStreamNonBlocking)) != hipSuccess) return e;
-        for (int k = 0; k < 4; k++)
-            if ((e = hipEventCreateWithFlags(&S.pev[k], hipEventDisableTiming)) != hipSuccess) return e;
+    if (table) {
+        e = lzf_launch_compress_table(b, s, S.p, S.cap);
+    } else {
+#ifdef LZF_DIAG
+        const char *ff = getenv("LZF_GPU_LANE_FORCE_FIX");
+        /* LZF_GPU_LANE_PIPE=1 overlaps the two kernels of consecutive chunks
+         * on two streams (both kernels hold LDS and do not co-reside well) */
+        const char *pp = getenv("LZF_GPU_LANE_PIPE");
+        const bool pipe = pp && *pp == '1';
+        if (pipe && !S.aux) {
+            if ((e = hipStreamCreateWithFlags(&S.aux, hipStreamNonBlocking)) != hipSuccess) return e;
+            for (int k = 0; k < 4; k++)
+                if ((e = hipEventCreateWithFlags(&S.pev[k], hipEventDisableTiming)) != hipSuccess) return e;
+        }
+        e = lzf_launch_compress_lane(b, s, S.p, S.cap, (ff && *ff == '1') ? 1u : 0u, pipe ? S.aux : nullptr,
+                                     pipe ? S.pev : nullptr);
+#else
+        e = lzf_launch_compress_lane(b, s, S.p, S.cap, 0u, nullptr, nullptr);
+#endif
     }
-    e = table ? lzf_launch_compress_table(b, s, S.p, S.cap)
-              : lzf_launch_compress_lane(b, s, S.p, S.cap, (ff && *ff == '1') ? 1u : 0u,
-                                         pipe ? S.aux : nullptr, pipe ? S.pev : nullptr);
     if (e != hipSuccess) return e;
     e = hipEventRecord(S.ev, s);
     S.last = s;
@@ -171,7 +196,9 @@ uint32_t lane_min_count(uint32_t max_len)
 hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
 {
     switch (kernel_gen()) {
+#ifdef LZF_DIAG
     case GEN_SERIAL: return lzf_launch_compress_serial(b, s);
+#endif
     case GEN_WINDOW: return lzf_launch_compress(b, s);
     case GEN_LANE:
         return (lzf_lane_compress_supported(b.max_len) && b.count >= lane_min_count(b.max_len))
@@ -198,24 +225,50 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
  * unless LZF_GPU_DECOMPRESS=lane asks for the lane decoder. */
 bool lane_decoder()
 {
+#ifdef LZF_DIAG
     const char *e = getenv("LZF_GPU_DECOMPRESS");
     return e && !strcmp(e, "lane");
+#else
+    return false;                    /* the lane decoder is in the diagnostic build only */
+#endif
 }
 
 hipError_t launch_decompress(const LzfBatch &b, hipStream_t s)
 {
     switch (kernel_gen()) {
+#ifdef LZF_DIAG
     case GEN_SERIAL: return lzf_launch_decompress_serial(b, s);
-    case GEN_WINDOW: return lzf_launch_decompress(b, s);
     default: return lane_decoder() ? lzf_launch_decompress_lane(b, s) : lzf_launch_decompress(b, s);
+#else
+    default: return lzf_launch_decompress(b, s);
+#endif
     }
 }
 
-[[noreturn]] void die(const char *what, hipError_t e)
+/* Library failures inside the host-memory paths are thrown as LzfFail and
+ * turned into an LZF_GPU_E* code at the C boundary (never abort: a transient
+ * HIP error must not take the server down). */
+struct LzfFail {
+    int code;
+};
+
+int code_of(hipError_t e)
 {
-    fprintf(stderr, "liblzf_hip: %s failed: %s -- no CPU fallback, aborting\n", what,
-            hipGetErrorString(e));
-    abort();
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return LZF_GPU_ENOMEM;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return LZF_GPU_ENODEV;
+    return LZF_GPU_ELAUNCH;
+}
+
+void check(hipError_t e, const char *what)
+{
+    if (e == hipSuccess) return;
+    static bool said = false;
+    if (!said) {
+        said = true;
+        fprintf(stderr, "liblzf_hip: %s failed: %s\n", what, hipGetErrorString(e));
+    }
+    (void)hipGetLastError();
+    throw LzfFail{code_of(e)};
 }
 
 struct DeviceGuard {
@@ -224,8 +277,7 @@ struct DeviceGuard {
     {
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
         if (prev != dev) {
-            hipError_t e = hipSetDevice(dev);
-            if (e != hipSuccess) die("hipSetDevice", e);
+            check(hipSetDevice(dev), "hipSetDevice");
         }
     }
     ~DeviceGuard()
@@ -249,9 +301,18 @@ struct Buf {
         p = nullptr;
         cap = 0;
         hipError_t e = pinned ? hipHostMalloc(&p, want, hipHostMallocDefault) : hipMalloc(&p, want);
-        if (e != hipSuccess) die(pinned ? "hipHostMalloc" : "hipMalloc", e);
+        if (e != hipSuccess) {
+            p = nullptr;
+            check(e, pinned ? "hipHostMalloc" : "hipMalloc");
+        }
         cap = want;
         return p;
+    }
+    void release()
+    {
+        if (p) { pinned ? (void)hipHostFree(p) : (void)hipFree(p); }
+        p = nullptr;
+        cap = 0;
     }
 };
 
@@ -274,6 +335,7 @@ struct Slot {
 
 struct Ctx {
     int dev = 0;
+    bool ok = false;
     hipStream_t stream = nullptr;
     Buf d_in, d_out, d_meta;
     Buf h_in{nullptr, 0, true}, h_out{nullptr, 0, true}, h_meta{nullptr, 0, true};
@@ -283,26 +345,41 @@ struct Ctx {
         const char *e = getenv("LZF_GPU_DEVICE");
         dev = e ? atoi(e) : 0;
         int n = 0;
-        if (hipGetDeviceCount(&n) != hipSuccess || dev >= n || !device_ok(dev)) {
-            fprintf(stderr, "liblzf_hip: no gfx950 device %d (devices: %d) -- no CPU fallback, aborting\n",
-                    dev, n);
-            abort();
+        if (hipGetDeviceCount(&n) != hipSuccess || dev < 0 || dev >= n || !device_ok(dev)) {
+            fprintf(stderr, "liblzf_hip: no gfx950 device %d (devices: %d); the codec runs on the GPU only\n", dev,
+                    n);
+            return;
         }
-        DeviceGuard g(dev);
-        hipError_t r = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
-        if (r != hipSuccess) die("hipStreamCreate", r);
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(dev);
+        ok = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess;
+        if (prev >= 0) (void)hipSetDevice(prev);
     }
+    /* the buffers of this thread (at its exit, or lzf_gpu_release) */
+    void release()
+    {
+        if (!ok) return;
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(dev);
+        if (stream) (void)hipStreamSynchronize(stream);
+        for (auto &sl : slot) {
+            if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+            for (Buf *b : {&sl.d_in, &sl.d_out, &sl.d_meta, &sl.h_in, &sl.h_out, &sl.h_meta}) b->release();
+            sl.busy = false;
+        }
+        for (Buf *b : {&d_in, &d_out, &d_meta, &h_in, &h_out, &h_meta}) b->release();
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    ~Ctx() { release(); }
 };
 
 Ctx &ctx()
 {
     static thread_local Ctx c;
+    if (!c.ok) throw LzfFail{LZF_GPU_ENODEV};
     return c;
-}
-
-void check(hipError_t e, const char *what)
-{
-    if (e != hipSuccess) die(what, e);
 }
 
 /* Run f(lo, hi) over [0, n) split into up to `threads` ranges. */
@@ -528,30 +605,69 @@ int host_batch(bool compress, const uint8_t *in, const uint64_t *in_off, const u
     return LZF_GPU_OK;
 }
 
+/* host_batch with the failure of a library call as a return code; the
+ * streams of the thread's context are drained so its buffers are free */
+int host_batch_rc(bool compress, const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                  uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len,
+                  int32_t *err, uint32_t count)
+{
+    try {
+        return host_batch(compress, in, in_off, in_len, out, out_off, out_cap, out_len, err, count);
+    } catch (const LzfFail &f) {
+        try {
+            Ctx &c = ctx();
+            if (c.stream) (void)hipStreamSynchronize(c.stream);
+            for (auto &sl : c.slot) {
+                if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+                sl.busy = false;
+            }
+            (void)hipGetLastError();
+        } catch (const LzfFail &) {
+        }
+        return f.code;
+    }
+}
+
 }  // namespace
 
 extern "C" {
 
+/* Single calls are batches of one.  A failure of the device path (no usable
+ * gfx950, a HIP error) is reported, never aborted on: lzf_compress returns 0,
+ * which the caller already reads as "store the value plain"
+ * (src/query.c:393-397); lzf_decompress returns 0 with errno EIO, an errno the
+ * reference codec never sets (src/lzf.h:85-91 lists E2BIG and EINVAL). */
 unsigned int lzf_compress(const void *const in_data, unsigned int in_len, void *out_data,
                           unsigned int out_len)
 {
     if (!in_len || !out_len) return 0;                    /* src/lzf_c.c:131 */
+    if (!in_data || !out_data) return 0;
     uint64_t zero = 0;
     uint32_t res = 0;
-    host_batch(true, (const uint8_t *)in_data, &zero, &in_len, (uint8_t *)out_data, &zero,
-               &out_len, &res, nullptr, 1);
-    return res;
+    const int rc = host_batch_rc(true, (const uint8_t *)in_data, &zero, &in_len, (uint8_t *)out_data, &zero,
+                                 &out_len, &res, nullptr, 1);
+    return rc == LZF_GPU_OK ? res : 0u;
 }
 
 unsigned int lzf_decompress(const void *const in_data, unsigned int in_len, void *out_data,
                             unsigned int out_len)
 {
+    uint8_t none = 0;
+    if (!in_data || (!out_data && out_len)) {             /* the reference would fault */
+        errno = EINVAL;
+        return 0;
+    }
+    if (!out_data) out_data = &none;                      /* out_len 0: nothing is written */
     uint64_t zero = 0;
     uint32_t res = 0;
     int32_t err = 0;
-    host_batch(false, (const uint8_t *)in_data, &zero, &in_len, (uint8_t *)out_data, &zero,
-               &out_len, &res, &err, 1);
-    if (!res) errno = err;
+    const int rc = host_batch_rc(false, (const uint8_t *)in_data, &zero, &in_len, (uint8_t *)out_data, &zero,
+                                 &out_len, &res, &err, 1);
+    if (rc != LZF_GPU_OK) {
+        errno = EIO;
+        return 0;
+    }
+    if (!res) errno = err ? err : EINVAL;
     return res;
 }
 
@@ -559,13 +675,14 @@ int lzf_gpu_compress_batch(const uint8_t *in, const uint64_t *in_off, const uint
                            uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
                            uint32_t *out_len, uint32_t count, uint32_t max_in_len, void *stream)
 {
-    if (!count || !in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len)
+    if (!count || !in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len || !max_in_len)
         return LZF_GPU_EARG;
     if (max_in_len > LZF_GPU_MAX_VALUE) return LZF_GPU_EARG;
     int rc = current_device_ok();
     if (rc) return rc;
     LzfBatch b{in, in_off, in_len, out, out_off, out_cap, out_len, nullptr, count, max_in_len};
-    return launch_compress(b, (hipStream_t)stream) == hipSuccess ? LZF_GPU_OK : LZF_GPU_ELAUNCH;
+    const hipError_t e = launch_compress(b, (hipStream_t)stream);
+    return e == hipSuccess ? LZF_GPU_OK : code_of(e);
 }
 
 int lzf_gpu_decompress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
@@ -578,7 +695,20 @@ int lzf_gpu_decompress_batch(const uint8_t *in, const uint64_t *in_off, const ui
     int rc = current_device_ok();
     if (rc) return rc;
     LzfBatch b{in, in_off, in_len, out, out_off, out_cap, out_len, err, count, max_out_cap};
-    return launch_decompress(b, (hipStream_t)stream) == hipSuccess ? LZF_GPU_OK : LZF_GPU_ELAUNCH;
+    const hipError_t e = launch_decompress(b, (hipStream_t)stream);
+    return e == hipSuccess ? LZF_GPU_OK : code_of(e);
+}
+
+void lzf_gpu_release(void)
+{
+    for (Scratch &S : g_scratch) {
+        std::lock_guard<std::mutex> lk(S.mu);
+        scratch_free(S);
+    }
+    try {
+        ctx().release();
+    } catch (const LzfFail &) {
+    }
 }
 
 int lzf_gpu_synth_fill(int kind, uint64_t seed, uint64_t first, uint64_t stride, uint32_t count,
@@ -597,14 +727,14 @@ int lzf_host_compress_batch(const uint8_t *in, const uint64_t *in_off, const uin
                             uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
                             uint32_t *out_len, uint32_t count)
 {
-    return host_batch(true, in, in_off, in_len, out, out_off, out_cap, out_len, nullptr, count);
+    return host_batch_rc(true, in, in_off, in_len, out, out_off, out_cap, out_len, nullptr, count);
 }
 
 int lzf_host_decompress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
                               uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
                               uint32_t *out_len, int32_t *err, uint32_t count)
 {
-    return host_batch(false, in, in_off, in_len, out, out_off, out_cap, out_len, err, count);
+    return host_batch_rc(false, in, in_off, in_len, out, out_off, out_cap, out_len, err, count);
 }
 
 uint64_t lzf_gpu_kv_frame_work_size(uint32_t count)
@@ -642,7 +772,9 @@ const char *lzf_gpu_kernel_info(void)
 {
     static thread_local std::string s;
     switch (kernel_gen()) {
+#ifdef LZF_DIAG
     case GEN_SERIAL: s = "compress=serial decompress=serial"; break;
+#endif
     case GEN_WINDOW:
         s = std::string("compress=") + lzf_compress_kernel_name() + " decompress=" +
             lzf_decompress_kernel_name();

@@ -147,7 +147,9 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
 {
     uint16_t *const T = L.T, *const Q = L.Q, *const O = L.O;
     uint32_t *const S = L.S;
+#if !KT_BALLOT
     unsigned long long *const Dw = L.Dw;
+#endif
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
     const uint32_t j = w - 1u;                                 /* worker's window (w >= 1) */
     const unsigned long long mine = 1ull << lane, below = mine - 1ull;
@@ -341,13 +343,13 @@ __global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt,
 #else
     __shared__ unsigned long long D[KT_WIN][144];                      /* slot digit bitmaps per worker */
 #endif
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
 #if !KT_BALLOT
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     unsigned long long *const Dw = D[w ? w - 1u : 0u];
 #endif
     const KtLds L{T, Q, O, S, Dw};
 #ifdef KT_PRIO
-    if (w == 0u) __builtin_amdgcn_s_setprio(KT_PRIO);   /* the table wave is the step's critical path */
+    if (threadIdx.x < 64u) __builtin_amdgcn_s_setprio(KT_PRIO);   /* the table wave */
 #endif
 #if !KT_BALLOT
     if (w)
@@ -355,7 +357,9 @@ __global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt,
 #endif
     for (uint32_t v = blockIdx.x; v < bt.count; v += gridDim.x) {
         const uint32_t n = bt.in_len[v];
-        if (n < 3u || n > LZF_SLOTS) continue;                  /* no positions (uniform per workgroup) */
+        /* no positions, or past the stated max_len (the record stride): the
+         * parse refuses such a value (uniform per workgroup) */
+        if (n < 3u || n > LZF_SLOTS || n > bt.max_len) continue;
         const uint8_t *src = bt.in + bt.in_off[v];
         uint32_t *rec = sc.rec + (uint64_t)v * sc.rstride;
         if (n >= 8u) kt_value<false>(L, src, n, rec);
@@ -397,7 +401,7 @@ __global__ __launch_bounds__(K3_THREADS) void lzf_parse_rec_kernel(LzfBatch bt, 
     const uint32_t v = blockIdx.x * K3_THREADS + threadIdx.x;
     if (v >= bt.count) return;
     const uint32_t n = bt.in_len[v], cap = bt.out_cap[v];
-    if (n == 0u || cap == 0u || n > LZF_SLOTS) {                   /* src/lzf_c.c:131 */
+    if (n == 0u || cap == 0u || n > LZF_SLOTS || n > bt.max_len) {  /* src/lzf_c.c:131; past max_len: refused */
         bt.out_len[v] = 0u;
         return;
     }

@@ -357,7 +357,9 @@ __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, ui
     const uint32_t cap = bt.out_cap[v];
     const uint8_t *src = bt.in + bt.in_off[v];
     uint8_t *dst = bt.out + bt.out_off[v];
-    if (n == 0u || cap == 0u) {                 /* src/lzf_c.c:131 */
+    /* src/lzf_c.c:131; a value past the batch's stated max_len (the LDS plan
+     * was sized from it) is refused the same way, never overrun */
+    if (n == 0u || cap == 0u || n > bt.max_len) {
         if (lane == 0) bt.out_len[v] = 0u;
         return;
     }

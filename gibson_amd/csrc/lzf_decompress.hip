@@ -122,6 +122,13 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
     const uint32_t cap = bt.out_cap[v];
     const uint8_t *src = bt.in + bt.in_off[v];
     uint8_t *dst = bt.out + bt.out_off[v];
+    if (cap > bt.max_len) {          /* past the batch's stated max_out_cap: refused, never overrun */
+        if (lane == 0) {
+            bt.out_len[v] = 0u;
+            bt.err[v] = 22;         /* EINVAL */
+        }
+        return;
+    }
     /* as the reference, a 0-length stream still reads its first control byte */
     const uint32_t avail = in_len ? in_len : 1u;
 

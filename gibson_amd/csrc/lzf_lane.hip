@@ -149,6 +149,7 @@ __device__ __forceinline__ uint32_t ln_slot(uint32_t tri)
 /* bijective 16-bit mix of the slot: bucket = high bits, identity = low bits */
 __device__ __forceinline__ uint32_t ln_mix(uint32_t s) { return (s * 40503u) & 0xFFFFu; }
 
+#ifdef LZF_DIAG   /* cross-check form, diagnostic build only */
 /* ======================================================================== */
 /* decompress: one lane per stream                                          */
 /* ======================================================================== */
@@ -236,6 +237,8 @@ __global__ __launch_bounds__(LD_THREADS) void lzf_decompress_lane_kernel(LzfBatc
     bt.err[v] = err;
 }
 
+#endif /* LZF_DIAG */
+
 /* Residency cap for the one-lane-per-value kernels: each lane streams its own
  * value, so the lines in use grow with the lanes in flight; past what the
  * XCD's L2 holds every access refetches its line.  Capping the blocks per CU
@@ -251,6 +254,7 @@ static size_t lane_lds_for(const char *env, uint32_t dflt_blocks_per_cu)
     return lds - 256u;
 }
 
+#ifdef LZF_DIAG
 hipError_t lzf_launch_decompress_lane(const LzfBatch &b, hipStream_t s)
 {
     const uint32_t grid = (b.count + LD_THREADS - 1u) / LD_THREADS;
@@ -263,6 +267,7 @@ hipError_t lzf_launch_decompress_lane(const LzfBatch &b, hipStream_t s)
     hipLaunchKernelGGL(lzf_decompress_lane_kernel, dim3(grid), dim3(LD_THREADS), lds, s, b);
     return hipGetLastError();
 }
+#endif /* LZF_DIAG */
 
 /* ======================================================================== */
 /* compress, kernel 1: same-slot predecessor of every position              */
@@ -319,6 +324,7 @@ __device__ __forceinline__ uint32_t k1_code(uint32_t k)
     return k < 3u ? CAND_DIFF : (k >= 8u ? CAND_LONG : k - 1u);
 }
 
+#ifdef LZF_DIAG   /* used by the mid class only */
 /* Lane-order check of the bucket-head atomics: a returned head from a later
  * position means the LDS did not serialise the wave's same-address atomics in
  * lane order; then the predecessors are rebuilt from the keys (the head before
@@ -354,6 +360,8 @@ __device__ __noinline__ void k1_fix_order(uint32_t (&r)[K1_WIN], const uint32_t 
     for (uint32_t j = 0; j < K1_WIN; j++)
         if (act[j]) r[j] = fixed[j];
 }
+
+#endif /* LZF_DIAG */
 
 /* Small class (every value <= MAXN <= 8 KiB bytes: all positions inside one
  * 8 KiB window, so no window test).  Persistent workgroups of one wave walk the batch; the next
@@ -429,7 +437,7 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                 pf[k] = at < pn ? ln_ld16_safe(s1 + at, pn - at) : make_uint4(0, 0, 0, 0);
             }
         }
-        if (n >= 3u) {
+        if (n >= 3u && n <= MAXN) {          /* a longer value: refused by the parse (n > max_len) */
             for (uint32_t k = lane; k < BUCKETS / 8u; k += 64u) ((uint4 *)H)[k] = make_uint4(0, 0, 0, 0);
             ln_wave_fence();
             const uint32_t np = n - 2u;               /* positions 0 .. n-3 */
@@ -546,6 +554,7 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
     }
 }
 
+#ifdef LZF_DIAG   /* ring and mid classes: cross-check forms */
 /* Small class, 16 KiB ("ring" form: values <= 16 KiB, so positions reach
  * 8 KiB past the window).  The value's bytes are staged whole as above; the
  * bucket heads are u32 [pos+1 | identity:4] (4096 buckets, 16 KiB) and the
@@ -853,6 +862,8 @@ __global__ __launch_bounds__(64) void lzf_cand_mid_kernel(LzfBatch bt, LzfLaneSc
     }
 }
 
+#endif /* LZF_DIAG */
+
 /* ======================================================================== */
 /* compress, kernel 2: the greedy parse and emission, one lane per value    */
 /* ======================================================================== */
@@ -909,7 +920,8 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
     const uint32_t v = blockIdx.x * K2_THREADS + threadIdx.x;
     if (v >= bt.count) return;
     const uint32_t n = bt.in_len[v], cap = bt.out_cap[v];
-    if (n == 0u || cap == 0u) { bt.out_len[v] = 0u; return; }        /* src/lzf_c.c:131 */
+    /* src/lzf_c.c:131; past the stated max_len (the scratch stride): refused */
+    if (n == 0u || cap == 0u || n > bt.max_len) { bt.out_len[v] = 0u; return; }
     const uint8_t *src = bt.in + bt.in_off[v];
     uint8_t *dst = bt.out + bt.out_off[v];
     const uint16_t *cand = sc.cand + (uint64_t)v * sc.cstride;
@@ -1200,6 +1212,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
 #undef K2_FLUSH_TO
 }
 
+#ifdef LZF_DIAG   /* wave-form parse: cross-check form */
 /* ======================================================================== */
 /* compress, kernel 2 (wave form): the parse 64 positions at a time         */
 /* ======================================================================== */
@@ -1503,6 +1516,8 @@ __global__ __launch_bounds__(64) void lzf_parse_wave_kernel(LzfBatch bt, LzfLane
 #undef KW_BYTE
 }
 
+#endif /* LZF_DIAG */
+
 /* ---- launcher ------------------------------------------------------------ */
 
 /* cand words per value: a multiple of 64 (128 bytes), so the parse's 64-byte
@@ -1518,25 +1533,31 @@ size_t lzf_lane_scratch_per_value(uint32_t max_len)
 /* The default lane path takes the small and ring classes (values <= 64 KiB;
  * LZF_GPU_LANE_RING=0 stops it at 8 KiB, and LZF_GPU_LANE_MID=1 then routes
  * values up to 64 KiB through the mid-class kernels). */
+#ifdef LZF_DIAG
 static bool lane_ring_enabled()
 {
     const char *r = getenv("LZF_GPU_LANE_RING");     /* "0" turns the ring class off */
     return !(r && *r == '0');
 }
+#endif
 
 bool lzf_lane_compress_supported(uint32_t max_len)
 {
+#ifndef LZF_DIAG
+    return max_len <= KS_MAXN;       /* the product library keeps the 4 KiB small class only */
+#else
     if (max_len <= KS8_MAXN) return true;
     if (max_len <= KR64_MAXN && lane_ring_enabled()) return true;
     const char *e = getenv("LZF_GPU_LANE_MID");
     return max_len <= KM_MAXN && e && *e == '1';
+#endif
 }
 
 hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scratch,
                                     size_t scratch_bytes, uint32_t force_fix, hipStream_t aux,
                                     hipEvent_t *ev)
 {
-    if (b.max_len > KM_MAXN) return hipErrorInvalidValue;
+    if (!lzf_lane_compress_supported(b.max_len)) return hipErrorInvalidValue;
     const uint64_t cstride = lane_cstride(b.max_len), bstride = lane_bstride(b.max_len);
     /* with an aux stream: two scratch halves, kernel 1 of chunk i+1 on s
      * overlaps kernel 2 of chunk i on aux */
@@ -1562,11 +1583,15 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
     }
     /* the small-class kernel is persistent: as many one-wave workgroups as
      * stay resident (LDS-bound), each walking the batch */
+#ifdef LZF_DIAG
     const bool ring = b.max_len > KS8_MAXN && b.max_len <= KR64_MAXN && lane_ring_enabled();
     const void *small_fn = b.max_len <= KS_MAXN    ? (const void *)lzf_cand_small_kernel<4u, KS_MAXN, KS_WIN>
                            : b.max_len <= KS8_MAXN ? (const void *)lzf_cand_small_kernel<3u, KS8_MAXN, KS8_WIN>
                            : b.max_len <= KR_MAXN  ? (const void *)lzf_cand_ring_kernel<KR_MAXN, KR_WIN>
                                                    : (const void *)lzf_cand_ring_kernel<KR64_MAXN, KR_WIN>;
+#else
+    const void *small_fn = (const void *)lzf_cand_small_kernel<4u, KS_MAXN, KS_WIN>;
+#endif
     uint32_t small_grid = 256u * 8u;
     {
         int dev = 0, cus = 0;
@@ -1585,8 +1610,10 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
     }
     /* kernel 2: one lane per value; LZF_GPU_LANE_PARSE=wave selects the wave
      * form for the small class (slower today) */
+#ifdef LZF_DIAG
     const char *pe = getenv("LZF_GPU_LANE_PARSE");
     const bool wave_parse = b.max_len <= KW_MAXN && pe && pe[0] == 'w';
+#endif
     const size_t parse_lds = lane_lds_for("LZF_LANE_PARSE_BLOCKS", 0u);
     if (parse_lds) {
         hipError_t e = hipFuncSetAttribute((const void *)lzf_parse_lane_kernel,
@@ -1610,7 +1637,9 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
         if (b.max_len <= KS_MAXN) {
             const uint32_t g = cnt < small_grid ? cnt : small_grid;
             hipLaunchKernelGGL((lzf_cand_small_kernel<4u, KS_MAXN, KS_WIN>), dim3(g), dim3(64), 0, s, c, sc[h]);
-        } else if (b.max_len <= KS8_MAXN) {
+        }
+#ifdef LZF_DIAG
+        else if (b.max_len <= KS8_MAXN) {
             const uint32_t g = cnt < small_grid ? cnt : small_grid;
             hipLaunchKernelGGL((lzf_cand_small_kernel<3u, KS8_MAXN, KS8_WIN>), dim3(g), dim3(64), 0, s, c, sc[h]);
         } else if (ring) {
@@ -1622,6 +1651,7 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
         } else {
             hipLaunchKernelGGL(lzf_cand_mid_kernel, dim3(cnt), dim3(64), 0, s, c, sc[h]);
         }
+#endif
         if ((e = hipGetLastError()) != hipSuccess) return e;
         hipStream_t s2 = s;
         if (pipe) {
@@ -1629,9 +1659,11 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
             if ((e = hipStreamWaitEvent(aux, ev[h], 0)) != hipSuccess) return e;
             s2 = aux;
         }
+#ifdef LZF_DIAG
         if (wave_parse)
             hipLaunchKernelGGL(lzf_parse_wave_kernel, dim3(cnt), dim3(64), 0, s2, c, sc[h]);
         else
+#endif
             hipLaunchKernelGGL(lzf_parse_lane_kernel, dim3((cnt + K2_THREADS - 1u) / K2_THREADS),
                                dim3(K2_THREADS), parse_lds, s2, c, sc[h]);
         if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -7,6 +7,7 @@ src/lzf_c.c:131/176/263/276); ``lzf_decompress(in, out_len)`` returns
 src/lzf_d.c:72-131.  There is no Python or CPU codec behind these names: a
 missing or unloadable library raises ``LzfLibraryMissing``.
 """
+import contextlib
 import ctypes
 import os
 
@@ -29,6 +30,7 @@ EXPORTS = (
     "lzf_gpu_kernel_info",
     "lzf_gpu_kv_frame_work_size",
     "lzf_gpu_kv_frame",
+    "lzf_gpu_release",
 )
 
 # item encodings (src/net.h:274-278) and the MGET reply code (src/query.h:71)
@@ -44,13 +46,40 @@ def lib_path():
     return os.path.join(_HERE, "liblzf_hip.so")
 
 
+def diag_lib_path():
+    """The diagnostic build (cross-check kernel forms; never the product)."""
+    return os.path.join(_HERE, "liblzf_hip_diag.so")
+
+
+_LOADED = {}
+
+
 def lib():
     """Load liblzf_hip.so (built in-tree by __graft_entry__.build())."""
     global _LIB
     if _LIB is not None:
         return _LIB
     # LZF_HIP_LIB: load a diagnostic build (e.g. liblzf_hip_stats.so) instead
-    path = os.environ.get("LZF_HIP_LIB") or lib_path()
+    _LIB = _load(os.environ.get("LZF_HIP_LIB") or lib_path())
+    return _LIB
+
+
+@contextlib.contextmanager
+def using(path):
+    """Route this module's calls through the library at ``path`` (e.g. the
+    diagnostic build) for the duration of the block."""
+    global _LIB
+    prev = _LIB
+    _LIB = _load(path)
+    try:
+        yield _LIB
+    finally:
+        _LIB = prev
+
+
+def _load(path):
+    if path in _LOADED:
+        return _LOADED[path]
     if not os.path.exists(path):
         raise LzfLibraryMissing(f"{path} not built: run __graft_entry__.build() "
                                 "(make -C gibson_amd/csrc); there is no CPU fallback")
@@ -73,6 +102,8 @@ def lib():
     L.lzf_host_compress_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32]
     L.lzf_host_decompress_batch.restype = ctypes.c_int
     L.lzf_host_decompress_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32]
+    L.lzf_gpu_release.restype = None
+    L.lzf_gpu_release.argtypes = []
     L.lzf_gpu_kernel_info.restype = ctypes.c_char_p
     L.lzf_gpu_kernel_info.argtypes = []
     L.lzf_gpu_kv_frame_work_size.restype = u64
@@ -81,12 +112,17 @@ def lib():
     L.lzf_gpu_kv_frame.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, ctypes.c_int,
                                    vp, u64, vp, vp, vp]
     del i32
-    _LIB = L
+    _LOADED[path] = L
     return L
 
 
 def kernel_info():
     return lib().lzf_gpu_kernel_info().decode()
+
+
+def release():
+    """lzf_gpu_release(): free the device scratch and this thread's staging."""
+    lib().lzf_gpu_release()
 
 
 def _check(rc, what):

@@ -15,7 +15,12 @@
  * the legacy default stream).  Calls are asynchronous on `stream`.
  *
  * Return value of every call: LZF_GPU_OK or a negative LZF_GPU_E* code
- * (the launch was not made).
+ * (the launch was not made).  Failures are returned, never aborted on.
+ *
+ * Bounds: a value longer than max_in_len (compress) or with an out_cap past
+ * max_out_cap (decompress) -- a caller that under-states the bound -- gets
+ * out_len 0 (and err EINVAL on decompress); nothing outside its own output
+ * range is written.
  */
 #ifndef LZF_GPU_H
 #define LZF_GPU_H
@@ -121,6 +126,11 @@ int lzf_gpu_kv_frame(const uint8_t *keys, const uint64_t *key_off, const uint32_
                      uint32_t elements, uint32_t max_val_len, int reply_header,
                      uint8_t *frame, uint64_t max_response, uint64_t *frame_len, void *work,
                      void *stream);
+
+/* Free the library's device scratch (all devices) and the calling thread's
+ * staging buffers; later calls allocate them again.  Each thread's staging
+ * buffers are also freed when the thread exits. */
+void lzf_gpu_release(void);
 
 /* Which kernel generation the batch calls dispatch to (diagnostics):
  * returns a static string such as "compress=window64 decompress=tokpar". */

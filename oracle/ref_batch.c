@@ -1,0 +1,41 @@
+/*
+ * ref_batch.c -- batch driver for the compiled reference codec (TEST
+ * INFRASTRUCTURE, oracle/_ref only): generates values with the synthetic
+ * generators (gibson_amd/csrc/synth.h) and compresses them with the
+ * reference's lzf_compress (src/lzf_c.c, built by oracle/Makefile as
+ * ref_lzf_compress), one value per OpenMP thread.  tests/golden/make_golden.py
+ * uses it for the full-batch digests of the BASELINE configs.
+ */
+#include <omp.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "synth.h"
+
+unsigned int ref_lzf_compress(const void *, unsigned int, void *, unsigned int);
+
+/* values first .. first+count-1 of (kind, seed), n bytes each; value k's
+ * stream at out + k*n, its length (0: does not fit) in lens[k];
+ * out_len = n - out_slack (the server's n-4 with out_slack 4, src/query.c:385) */
+int ref_batch_compress(int kind, uint64_t seed, uint64_t first, uint32_t count, uint32_t n,
+                       uint32_t out_slack, uint8_t *out, uint32_t *lens, int threads)
+{
+    if (threads > 0) omp_set_num_threads(threads);
+    int bad = 0;
+#pragma omp parallel
+    {
+        uint8_t *buf = (uint8_t *)__builtin_malloc(n + 16);
+        if (!buf) {
+#pragma omp atomic write
+            bad = 1;
+        } else {
+#pragma omp for schedule(static)
+            for (uint32_t k = 0; k < count; k++) {
+                syn_generate(kind, seed, first + k, buf, n);
+                lens[k] = ref_lzf_compress(buf, n, out + (uint64_t)k * n, n - out_slack);
+            }
+            __builtin_free(buf);
+        }
+    }
+    return bad ? -1 : 0;
+}

@@ -16,6 +16,11 @@ Files:
   corpus.json  randomized compress cases over kinds x sizes x out_len regimes
                (incl. the exact success/failure boundary), plus decoder cases
                (valid streams, truncations, corruptions, tight out_len)
+  digests.json full-batch digests of the BASELINE configs' generators: the
+               first 64 K values of configs[1..4] (and all 256 K of configs[2])
+               compressed by the reference at out_len = n-4 (src/query.c:385);
+               digest = sha256 over the values in order of (u32 LE length ||
+               stream), a length of 0 = does not fit (tests/digest.py)
 """
 import ctypes
 import errno
@@ -150,13 +155,66 @@ def corpus():
     return comp, dec
 
 
+# (BASELINE config, kind, seed, n, count) -- tests/digest.py holds the same
+DIGEST_CONFIGS = [
+    (1, 1, 0x5EED0002, 4096, 65536),
+    (2, 2, 0x5EED0003, 65536, 65536),
+    (2, 2, 0x5EED0003, 65536, 262144),
+    (3, 0, 0x5EED0004, 8192, 65536),
+    (4, 3, 0x5EED0005, 16384, 65536),
+]
+
+
+def digests():
+    import numpy as np
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libref_batch.so"))
+    lib.ref_batch_compress.restype = ctypes.c_int
+    lib.ref_batch_compress.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                       ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_int]
+    res = []
+    for cfg, kind, seed, n, count in DIGEST_CONFIGS:
+        h = hashlib.sha256()
+        chunk = max(1, min(count, (512 << 20) // n))
+        out = np.empty(chunk * n, np.uint8)
+        lens = np.empty(chunk, np.uint32)
+        total = comp = 0
+        for first in range(0, count, chunk):
+            m = min(chunk, count - first)
+            rc = lib.ref_batch_compress(kind, seed, first, m, n, 4, out.ctypes.data, lens.ctypes.data,
+                                        os.cpu_count() or 1)
+            assert rc == 0
+            for k in range(m):
+                ln = int(lens[k])
+                h.update(ln.to_bytes(4, "little"))
+                h.update(out[k * n:k * n + ln].tobytes())
+                comp += ln
+            total += m
+        res.append({"config": cfg, "kind": kind, "seed": seed, "n": n, "first": 0, "count": count,
+                    "out_len": "n-4", "sha256": h.hexdigest(), "comp_bytes": comp})
+        print("digest", cfg, n, count, h.hexdigest()[:16], comp / (count * n))
+    return res
+
+
 def main():
     here = os.path.dirname(os.path.abspath(__file__))
+    if len(sys.argv) > 1 and sys.argv[1] == "digests":
+        with open(os.path.join(here, "digests.json"), "w") as f:
+            json.dump({"generator": "tests/golden/make_golden.py digests",
+                       "source": "oracle/_ref/libref_batch.so (reference lzf_c.c)",
+                       "record": "sha256 over values in order of u32 LE length || stream",
+                       "digests": digests()}, f, indent=1)
+        return 0
     k = kat()
     with open(os.path.join(here, "kat.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py", "source": "oracle/_ref/liblzf_ref.so",
                    "cases": k}, f, indent=0)
     c, d = corpus()
+    with open(os.path.join(here, "digests.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py digests",
+                   "source": "oracle/_ref/libref_batch.so (reference lzf_c.c)",
+                   "record": "sha256 over values in order of u32 LE length || stream",
+                   "digests": digests()}, f, indent=1)
     with open(os.path.join(here, "corpus.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py", "source": "oracle/_ref/liblzf_ref.so",
                    "E2BIG": errno.E2BIG, "EINVAL": errno.EINVAL,

@@ -99,3 +99,34 @@ def test_differential_vs_reference(oracle):
             b[rnd.randrange(len(b))] = rnd.randrange(256)
             b = bytes(b[:rnd.randint(0, len(b))])
             assert oracle.decompress(b, n + 10) == ref.decompress(b, n + 10)
+
+
+def test_oracle_matches_full_batch_digest():
+    # the clean-room restatement against the reference's whole-batch digest of
+    # BASELINE configs[1] (64 K JSON-like values of 4 KiB, out_len = n-4)
+    import ctypes
+    import json
+    import os
+
+    import numpy as np
+
+    from tests.digest import batch_digest
+    d = [x for x in json.load(open(os.path.join(oracle_lib.ROOT, "tests", "golden", "digests.json")))["digests"]
+         if x["config"] == 1][0]
+    n, count = d["n"], d["count"]
+    syn = ctypes.CDLL(os.path.join(oracle_lib.ROOT, "gibson_amd", "libgibson_synth.so"))
+    syn.synth_fill.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                               ctypes.c_uint32, ctypes.c_void_p]
+    src = np.empty(count * n, np.uint8)
+    syn.synth_fill(d["kind"], d["seed"], 0, count, n, src.ctypes.data)
+    L = ctypes.CDLL(oracle_lib.ORACLE_SO)
+    vp = ctypes.c_void_p
+    L.oracle_compress_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, ctypes.c_int]
+    offs = np.arange(count, dtype=np.uint64) * n
+    ln = np.full(count, n, np.uint32)
+    cap = np.full(count, n - 4, np.uint32)
+    out = np.empty(count * n, np.uint8)
+    olen = np.empty(count, np.uint32)
+    L.oracle_compress_batch(src.ctypes.data, offs.ctypes.data, ln.ctypes.data, count, out.ctypes.data,
+                            offs.ctypes.data, cap.ctypes.data, olen.ctypes.data, 1)
+    assert batch_digest(out, n, olen) == d["sha256"]
