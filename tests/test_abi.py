@@ -23,8 +23,17 @@ def test_headers_declare_the_reference_pair():
     assert 'extern "C"' in src
 
 
+def _declared_gb():
+    src = open(os.path.join(ROOT, "include", "gb_batch.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return set(re.findall(r"\b(gb_\w+)\s*\(", src))
+
+
 def test_library_exports_every_declared_symbol():
     L = gibson_amd.lib()
+    for n in sorted(_declared_gb()):
+        assert hasattr(L, n), n
+    assert len(_declared_gb()) == 9
     names = _declared("lzf.h") | _declared("lzf_gpu.h")
     for n in sorted(names):
         assert hasattr(L, n), n
