@@ -443,6 +443,15 @@ __global__ __launch_bounds__(K3_THREADS) void lzf_parse_rec_kernel(LzfBatch bt, 
     uint32_t reln = 0u, qn = 0u;       /* the next chain link from the same record (reln 0: none) */
     bool ok = true;
     uint32_t mode = n >= 3u ? K3_STEP : K3_DONE;
+#ifdef KT_TIMING
+    /* [8] wave iterations [9] wave cycles [10] steps [11] resolve tests
+     * [12] bitmap words from scratch [13] record hops [14] extend pieces [15] block loads */
+    uint64_t k3c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t k3t0 = __builtin_amdgcn_s_memtime();
+#define K3_CNT(i) (k3c[(i) - 8]++)
+#else
+#define K3_CNT(i) ((void)0)
+#endif
 
 #define K3_PUT(bytes_, cnt_)                                                       \
     do {                                                                           \
@@ -508,13 +517,16 @@ __global__ __launch_bounds__(K3_THREADS) void lzf_parse_rec_kernel(LzfBatch bt, 
     } while (0)
 
     while (__ballot(mode != K3_DONE)) {
+        K3_CNT(8);
         /* ---- the record of p ---------------------------------------------- */
         if (mode == K3_STEP) {                                            /* src/lzf_c.c:145 */
             if (p >= n - 2u) {
                 mode = K3_DONE;
             } else {
+                K3_CNT(10);
                 uint32_t d = p - cb;
                 if (d >= K3_CB) {
+                    K3_CNT(15);
                     cb = p & ~(K3_CB - 1u);
                     d = p - cb;
                     const uint4 *cp = (const uint4 *)(rec + cb);
@@ -540,12 +552,16 @@ __global__ __launch_bounds__(K3_THREADS) void lzf_parse_rec_kernel(LzfBatch bt, 
         }
         /* ---- is the candidate inserted? else the next chain link ---------- */
         if (mode == K3_RESOLVE) {
+            K3_CNT(11);
             uint32_t word;
             if (q >= ms) {
                 word = (q > ms && q + 3u <= me) ? 0u : 0xFFFFFFFFu;         /* last match's interior */
             } else {
                 const uint32_t d = cw - (q >> 5);
                 word = d == 0u ? curw : (q >> 5) >= fl ? K3_RING(q >> 5) : bits[q >> 5];
+#ifdef KT_TIMING
+                if (d && (q >> 5) < fl) K3_CNT(12);
+#endif
             }
             if ((word >> (q & 31u)) & 1u) {                              /* q is the ref */
                 if (rel == 9u)
@@ -560,6 +576,7 @@ __global__ __launch_bounds__(K3_THREADS) void lzf_parse_rec_kernel(LzfBatch bt, 
                  * qn = q (a load below on the next failure) */
                 qn = 0xFFFFFFFFu;
             } else if (qn == 0xFFFFFFFFu) {                              /* load q's record: two more links */
+                K3_CNT(13);
                 const uint32_t c2 = rec[q];
                 const uint32_t r1 = (c2 >> 13) & 7u, r2 = c2 >> 29;
                 const uint32_t y1 = q - 1u - (c2 & 0x1FFFu), y2 = q - 1u - ((c2 >> 16) & 0x1FFFu);
@@ -618,6 +635,7 @@ __global__ __launch_bounds__(K3_THREADS) void lzf_parse_rec_kernel(LzfBatch bt, 
         /* ---- one 16-byte piece of a long match ----------------------------- */
         if (mode == K3_EXTEND) {
             if (k < lim) {
+                K3_CNT(14);
                 const uint32_t avail = n - (p + k);
                 const uint4 a = dv_ld16_safe(src + p + k, avail), b = dv_ld16_safe(src + q + k, avail);
                 W = a;                                   /* literals after the match read it */
@@ -680,6 +698,12 @@ __global__ __launch_bounds__(K3_THREADS) void lzf_parse_rec_kernel(LzfBatch bt, 
             }
         }
     }
+#ifdef KT_TIMING
+    k3c[1] = __builtin_amdgcn_s_memtime() - k3t0;
+    if ((threadIdx.x & 63u) != 0u) k3c[0] = k3c[1] = 0u;   /* wave figures once */
+    for (uint32_t i = 0; i < 8u; i++) atomicAdd(&kt_times[8u + i], (unsigned long long)k3c[i]);
+#endif
+#undef K3_CNT
     if (!ok || o + 3u > cap) { bt.out_len[v] = 0u; return; }          /* src/lzf_c.c:276 */
     while (p < n) {                                                   /* src/lzf_c.c:279-288 */
         K3_LITERAL(p);

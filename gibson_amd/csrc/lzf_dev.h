@@ -66,6 +66,23 @@ __device__ __forceinline__ uint2 dv_ld8_clamped(const uint8_t *src, uint32_t n, 
     return make_uint2((uint32_t)y, (uint32_t)(y >> 32));
 }
 
+/* the 16-byte load address for bytes from pp in a value of n >= 16 bytes:
+ * moved back to n - 16 near the end, so the load stays inside the value */
+__device__ __forceinline__ uint32_t dv_at16(uint32_t n, uint32_t pp) { return pp + 16u <= n ? pp : n - 16u; }
+
+/* v shifted down by sh (0 .. 15) bytes, zeros in */
+__device__ __forceinline__ uint4 dv_shr16(uint4 v, uint32_t sh)
+{
+    uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
+    const bool big = sh >= 8u;
+    lo = big ? hi : lo;
+    hi = big ? 0ull : hi;
+    const uint32_t b = 8u * (sh & 7u);
+    lo = b ? (lo >> b) | (hi << (64u - b)) : lo;
+    hi >>= b;
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+
 /* slot(p) of src/lzf_c.c:47-57 (VERY_FAST, HLOG 16) from b[p..p+2] = tri */
 __device__ __forceinline__ uint32_t dv_slot(uint32_t tri)
 {

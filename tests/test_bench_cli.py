@@ -35,3 +35,34 @@ def test_bench_small_run(args):
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["config"]["roundtrip_ok"] is True
     assert line["value"] > 0 and line["roofline"]["peak"] == 8000.0
+
+
+def test_bench_gpus_must_match_world_size():
+    # under torchrun, --gpus N that disagrees with WORLD_SIZE is refused
+    # before any GPU work
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode != 0
+    assert "WORLD_SIZE" in r.stderr
+
+
+@pytest.mark.gpu
+def test_bench_default_is_configs2_with_cpu_baseline():
+    # the driver's N=1 command on the default workload: BASELINE configs[2]
+    # (256K x 64 KiB text), the CPU baseline on every core this process may
+    # use plus a 1-core figure
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "1",
+                        "--warmup", "0", "--cpu-count", "64"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-800:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["config"]["baseline_config"] == 2
+    assert line["config"]["workload"].startswith("256K x 64 KiB") and line["n_gpus"] == 1
+    assert line["config"]["roundtrip_ok"] is True
+    cb = line["cpu_baseline"]
+    assert cb["cores"] == bench.cpu_cores()[0]
+    assert cb["value_1core"] > 0 and cb["value"] > 0

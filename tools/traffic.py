@@ -18,7 +18,7 @@ import json
 import sys
 
 GROUPS = {
-    "lzf_compress": ("compress_window", "compress_serial", "lzf_cand_", "lzf_parse_lane"),
+    "lzf_compress": ("compress_window", "compress_serial", "lzf_cand_", "lzf_parse_lane", "lzf_parse_rec"),
     "lzf_decompress": ("decompress",),
 }
 
