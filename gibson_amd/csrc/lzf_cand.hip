@@ -269,13 +269,19 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 ak[PS] = a;
                 const uint32_t s = dv_slot(a.x);
 #if KT_BALLOT
-                /* exact: the lanes agreeing with mine on every slot bit */
-                unsigned long long M = __ballot(act);
+                /* exact: the lanes agreeing with mine on every slot bit.  Per
+                 * bit: x = my bit sign-extended (0 / ~0), its ballot bb, and
+                 * M &= ~(bb ^ x) as one v_bitop3 per half (4 VALU per bit) */
+                const unsigned long long M0 = __ballot(act);
+                uint32_t mlo = (uint32_t)M0, mhi = (uint32_t)(M0 >> 32);
 #pragma unroll
                 for (uint32_t b = 0; b < 16u; b++) {
-                    const unsigned long long bb = __ballot((s >> b) & 1u);
-                    M &= ((s >> b) & 1u) ? bb : ~bb;
+                    const uint32_t x = (uint32_t)((int32_t)(s << (31u - b)) >> 31);
+                    const unsigned long long bb = __ballot(x != 0u);
+                    mlo = __builtin_amdgcn_bitop3_b32(mlo, (uint32_t)bb, x, 0x90);
+                    mhi = __builtin_amdgcn_bitop3_b32(mhi, (uint32_t)(bb >> 32), x, 0x90);
                 }
+                unsigned long long M = ((unsigned long long)mhi << 32) | mlo;
                 if (!act) M = 0ull;
 #else
                 const uint32_t i0 = s & 63u, i1 = 64u + ((s >> 6) & 63u), i2 = 128u + (s >> 12);
@@ -371,9 +377,13 @@ __global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt,
 /* kernel 2: the greedy parse and emission, one lane per value              */
 /* ======================================================================== */
 
+#ifndef K3_THREADS
 #define K3_THREADS 256u
+#endif
 #define K3_CB      16u          /* records per parse block: 64 bytes of one line */
+#ifndef K3_RW
 #define K3_RW      32u          /* bitmap words kept in LDS per lane (power of two) */
+#endif
 
 /* rel codes of the walk, relative to p: the record codes 0..7, plus
  * 8 (the first 3 bytes agree, length unknown) and 9 (unknown) */

@@ -9,5 +9,5 @@ src=${SRC:-lzf_lane.hip}
 cd "$(dirname "$0")/../gibson_amd/csrc"
 H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -munsafe-fp-atomics -I. -I../../include"
 $H "$@" -c "$src" -o build/var_$name.o
-$H -shared -o ../liblzf_hip_$name.so build/var_$name.o $(ls build/*.o | grep -v -e "build/${src%.hip}.o" -e var_ -e stats_ -e diag_ -e lzf_serial.o)
+$H -shared -o ../liblzf_hip_$name.so build/var_$name.o $(ls build/*.o | grep -v -e "build/${EXCL:-${src%.hip}.o}" -e var_ -e stats_ -e diag_ -e lzf_serial.o)
 echo built gibson_amd/liblzf_hip_$name.so
