@@ -162,8 +162,17 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
     uint2 pf[KT_PF], ak[KT_PF];
 #pragma unroll
     for (uint32_t d = 0; d < KT_PF; d++) {
-        pf[d] = w ? kt_ld8<SMALL>(src, n, KT_BLK * d + 64u * j + lane) : make_uint2(0u, 0u);
+        pf[d] = make_uint2(0u, 0u);
         ak[d] = make_uint2(0u, 0u);
+    }
+    if (w) {
+        if (!SMALL && KT_BLK * KT_PF + 8u <= n) {                /* the first blocks need no clamp */
+#pragma unroll
+            for (uint32_t d = 0; d < KT_PF; d++) pf[d] = dv_ld8(src + KT_BLK * d + 64u * j + lane);
+        } else {
+#pragma unroll
+            for (uint32_t d = 0; d < KT_PF; d++) pf[d] = kt_ld8<SMALL>(src, n, KT_BLK * d + 64u * j + lane);
+        }
     }
     /* the table starts empty for every value (position 0 = none: it is
      * never a ref, and a candidate 0 decides like no candidate) */
@@ -175,8 +184,12 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
 #ifdef KT_TIMING
     uint64_t kt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-    const auto step = [&](auto ps, uint32_t t) {
+    const auto step = [&](auto ps, auto clamp, uint32_t t) {
         constexpr uint32_t PS = decltype(ps)::value;             /* t % KT_PF */
+        /* CLAMP: the step's loads may reach past the value (its last
+         * blocks); otherwise they are plain 8-byte loads */
+        constexpr bool CLAMP = SMALL || decltype(clamp)::value != 0u;
+        const auto ld8 = [&](uint32_t pp) { return CLAMP ? kt_ld8<SMALL>(src, n, pp) : dv_ld8(src + pp); };
         KT_T0();
         /* this step's global loads are issued unconditionally, by every
          * wave, at the end: a load inside a branch leaves a register merge
@@ -313,9 +326,9 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
 #ifdef KT_ABL_C
         l1 = l2 = 0u;
 #endif
-        c_b1 = kt_ld8<SMALL>(src, n, l1);
-        c_b2 = kt_ld8<SMALL>(src, n, l2);
-        pf[PS] = kt_ld8<SMALL>(src, n, lp);
+        c_b1 = ld8(l1);
+        c_b2 = ld8(l2);
+        pf[PS] = ld8(lp);
         if (w) KT_TM(5);
 #ifndef KT_ABL_S
         __syncthreads();
@@ -326,11 +339,22 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
         kt_acc[7]++;
 #endif
     };
-    for (uint32_t t = 0; t < nb + 3u; t += KT_PF) {
-        step(KtIc<0>{}, t);
-        step(KtIc<1>{}, t + 1u);
-        step(KtIc<2>{}, t + 2u);
-        step(KtIc<3>{}, t + 3u);
+    /* steps whose loads all stay inside the value -- the input of block
+     * t + KT_PF and agreement bytes of positions before block t - 1 -- skip
+     * the end-of-value clamp (the last group of steps keeps it) */
+    uint32_t t = 0;
+    if (!SMALL)
+        for (; t < nb + 3u && KT_BLK * (t + 3u + KT_PF + 1u) + 8u <= n; t += KT_PF) {
+            step(KtIc<0>{}, KtIc<0>{}, t);
+            step(KtIc<1>{}, KtIc<0>{}, t + 1u);
+            step(KtIc<2>{}, KtIc<0>{}, t + 2u);
+            step(KtIc<3>{}, KtIc<0>{}, t + 3u);
+        }
+    for (; t < nb + 3u; t += KT_PF) {
+        step(KtIc<0>{}, KtIc<1>{}, t);
+        step(KtIc<1>{}, KtIc<1>{}, t + 1u);
+        step(KtIc<2>{}, KtIc<1>{}, t + 2u);
+        step(KtIc<3>{}, KtIc<1>{}, t + 3u);
     }
 #ifdef KT_TIMING
     if (lane == 0u)
