@@ -289,7 +289,8 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 uint32_t mlo = (uint32_t)M0, mhi = (uint32_t)(M0 >> 32);
 #pragma unroll
                 for (uint32_t b = 0; b < 16u; b++) {
-                    const uint32_t x = (uint32_t)((int32_t)(s << (31u - b)) >> 31);
+                    uint32_t x;                          /* v_bfe_i32: the compiler would split it */
+                    asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(x) : "v"(s), "n"(b));
                     const unsigned long long bb = __ballot(x != 0u);
                     mlo = __builtin_amdgcn_bitop3_b32(mlo, (uint32_t)bb, x, 0x90);
                     mhi = __builtin_amdgcn_bitop3_b32(mhi, (uint32_t)(bb >> 32), x, 0x90);
