@@ -38,10 +38,12 @@ namespace {
 enum KernelGen { GEN_TABLE = 0, GEN_LANE = 1, GEN_WINDOW = 2, GEN_SERIAL = 3 };
 
 /* LZF_GPU_KERNEL picks the kernel generation, read per launch so one process
- * can A/B them: "lane" (default; one lane per value, lzf_lane.hip),
- * "window" (one wave per value: window64 / tokpar64) or "serial" (the
- * single-lane first generation).  All are bit-exact; the GPU tests
- * cross-check them. */
+ * can A/B them.  Unset: the measured routing of launch_compress (the table
+ * generation, lzf_cand.hip, for values of 4-64 KiB; the lane small class,
+ * lzf_lane.hip, up to 4 KiB; window64 past 64 KiB and for small batches).
+ * "lane": the lane generation wherever it applies; "window": one wave per
+ * value (window64 / tokpar64); "serial" (diagnostic build): the single-lane
+ * first generation.  All are bit-exact; the GPU tests cross-check them. */
 KernelGen kernel_gen()
 {
     const char *e = getenv("LZF_GPU_KERNEL");
