@@ -181,18 +181,22 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s, bool table)
     return e;
 }
 
-/* smallest batch the lane generation takes (LZF_GPU_LANE_MIN overrides):
- * tools/crossover.py measured the crossover near 160 k values of 4 KiB,
- * near 48 k values of 8 KiB (window64 is 2.2x slower per byte there) and
- * near 160 k values of 16 KiB (mixed entropy: 86.0 vs 82.0 ms at 128 K,
- * 136.8 vs 163.8 ms at 256 K) and near 96 k values of 64 KiB (sentence
- * text: 172.4 vs 164.9 ms at 64 K, 261.6 vs 327.6 ms at 128 K) */
+/* smallest batch the lane / table generations take (LZF_GPU_LANE_MIN
+ * overrides): below it window64's one wave per value finishes first, since
+ * the parse's time has a floor of one whole value's parse per lane.
+ * tools/crossover.py, table generation vs window64 (ms): 8 KiB text 11.6 vs
+ * 5.8 at 16 K values, 15.5 vs 22.4 at 64 K; 16 KiB mixed 44.0 vs 41.4 at
+ * 64 K, 54.5 vs 82.3 at 128 K; 64 KiB text 94.2 vs 50.5 at 16 K, 116.8 vs
+ * 197.3 at 64 K (profiles/r02/crossover_table.txt).  The 4 KiB lane small
+ * class: near 160 K values (round 1). */
 uint32_t lane_min_count(uint32_t max_len)
 {
     const char *e = getenv("LZF_GPU_LANE_MIN");
     if (e) return (uint32_t)strtoul(e, nullptr, 10);
-    if (max_len > 16384u) return 98304u;
-    return (max_len > 4096u && max_len <= 8192u) ? 49152u : 163840u;
+    if (max_len <= 4096u) return 163840u;
+    if (max_len <= 8192u) return 40960u;
+    if (max_len <= 16384u) return 81920u;
+    return 32768u;
 }
 
 hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
