@@ -969,29 +969,35 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
     bool ok = true;
     uint32_t mode = n >= 3u ? K2_STEP : K2_DONE;
 
+/* completed dwords [fs, fw) wait in pb0..2 (slot fw - fs) and leave with
+ * the fourth as one 16-byte store; slot and patch selects instead of
+ * branches (lzf_cand.hip's parse has the same cursor) */
+#define K2_STORE16(w_)                                                             \
+    do {                                                                           \
+        if (fs == 0u && dm != 0u) {        /* dst's first dword: bytes before dst are not ours */ \
+            for (uint32_t t_ = dm; t_ < 4u; t_++) da[t_] = (uint8_t)(pb0 >> (8u * t_)); \
+            const uint2 m_ = make_uint2(pb1, pb2);                                 \
+            __builtin_memcpy(da + 4u, &m_, 8);                                     \
+            const uint32_t l_ = (w_);                                              \
+            __builtin_memcpy(da + 12u, &l_, 4);                                    \
+        } else {                                                                   \
+            const uint4 v_ = make_uint4(pb0, pb1, pb2, (w_));                      \
+            __builtin_memcpy(da + 4u * fs, &v_, 16);                               \
+        }                                                                          \
+        K2_SITE(8);                                                                \
+    } while (0)
 #define K2_PUT(bytes_, cnt_)                                                       \
     do {                                                                           \
         acc |= (uint64_t)(bytes_) << (8u * accn);                                  \
         accn += (cnt_);                                                            \
         if (accn >= 4u) {                                                          \
-            const uint32_t w_ = (uint32_t)acc;                                     \
-            if (fw == 0u && dm != 0u) {        /* the partial first dword */       \
-                for (uint32_t t_ = dm; t_ < 4u; t_++) da[t_] = (uint8_t)(w_ >> (8u * t_)); \
-                fs = 1u;                                                           \
-            } else {                                                               \
-                const uint32_t np_ = fw - fs;                                      \
-                if (np_ == 3u) {                                                   \
-                    const uint4 v_ = make_uint4(pb0, pb1, pb2, w_);                \
-                    __builtin_memcpy(da + 4u * fs, &v_, 16);                       \
-                    K2_SITE(8);                                                    \
-                    fs = fw + 1u;                                                  \
-                } else if (np_ == 0u) {                                            \
-                    pb0 = w_;                                                      \
-                } else if (np_ == 1u) {                                            \
-                    pb1 = w_;                                                      \
-                } else {                                                           \
-                    pb2 = w_;                                                      \
-                }                                                                  \
+            const uint32_t w_ = (uint32_t)acc, np_ = fw - fs;                      \
+            pb0 = np_ == 0u ? w_ : pb0;                                            \
+            pb1 = np_ == 1u ? w_ : pb1;                                            \
+            pb2 = np_ == 2u ? w_ : pb2;                                            \
+            if (np_ == 3u) {                                                       \
+                K2_STORE16(w_);                                                    \
+                fs = fw + 1u;                                                      \
             }                                                                      \
             fw++;                                                                  \
             acc >>= 32;                                                            \
@@ -1006,9 +1012,9 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
         } else if ((x_) >= 4u * fs) {                                              \
             const uint32_t i_ = ((x_) >> 2) - fs, sh_ = 8u * ((x_) & 3u);          \
             const uint32_t mk_ = ~(0xFFu << sh_), b_ = (uint32_t)(byte_) << sh_;  \
-            if (i_ == 0u) pb0 = (pb0 & mk_) | b_;                                  \
-            else if (i_ == 1u) pb1 = (pb1 & mk_) | b_;                             \
-            else pb2 = (pb2 & mk_) | b_;                                           \
+            pb0 = i_ == 0u ? (pb0 & mk_) | b_ : pb0;                               \
+            pb1 = i_ == 1u ? (pb1 & mk_) | b_ : pb1;                               \
+            pb2 = i_ == 2u ? (pb2 & mk_) | b_ : pb2;                               \
         } else {                                                                   \
             da[(x_)] = (uint8_t)(byte_);                                           \
         }                                                                          \
@@ -1028,8 +1034,9 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
     do {                                                                           \
         uint32_t byte_;                                                            \
         K2_BYTE(pos_, byte_);                                                      \
-        if (run == 0u) { hx = 4u * fw + accn; K2_PUT(byte_ << 8, 2u); }           \
-        else K2_PUT(byte_, 1u);                                                    \
+        const bool first_ = run == 0u;             /* the run's header slot first */ \
+        hx = first_ ? 4u * fw + accn : hx;                                         \
+        K2_PUT(first_ ? byte_ << 8 : byte_, first_ ? 2u : 1u);                     \
         o++;                                                                       \
         if (++run == LZF_MAX_LIT) { K2_PATCH(hx, LZF_MAX_LIT - 1u); run = 0u; o++; } \
     } while (0)
@@ -1153,13 +1160,11 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                 mode = K2_DONE;
             } else {
                 const uint32_t L = m - 2u;
-                if (L < 7u) {
-                    K2_PUT(((off >> 8) | (L << 5)) | ((off & 0xFFu) << 8), 2u);
-                    o += 2u;
-                } else {
-                    K2_PUT((0xE0u | (off >> 8)) | ((L - 7u) << 8) | ((off & 0xFFu) << 16), 3u);
-                    o += 3u;
-                }
+                const bool two = L < 7u;
+                K2_PUT(two ? ((off >> 8) | (L << 5)) | ((off & 0xFFu) << 8)
+                           : (0xE0u | (off >> 8)) | ((L - 7u) << 8) | ((off & 0xFFu) << 16),
+                       two ? 2u : 3u);
+                o += two ? 2u : 3u;
                 run = 0u;
                 o++;                                                     /* reserve a header */
                 ms = p;
@@ -1199,11 +1204,17 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
     }
     if (run) K2_PATCH(hx, run - 1u);
     else o--;
-    for (uint32_t i = fs; i < fw; i++)
-        *(uint32_t *)(da + 4u * i) = i == fs ? pb0 : i == fs + 1u ? pb1 : pb2;
+    for (uint32_t i = fs; i < fw; i++) {
+        const uint32_t wv = i == fs ? pb0 : i == fs + 1u ? pb1 : pb2;
+        if (i == 0u && dm != 0u)
+            for (uint32_t t = dm; t < 4u; t++) da[t] = (uint8_t)(wv >> (8u * t));
+        else
+            *(uint32_t *)(da + 4u * i) = wv;
+    }
     for (uint32_t t = 0; t < accn; t++)
         if (4u * fw + t >= dm) da[4u * fw + t] = (uint8_t)(acc >> (8u * t));
     bt.out_len[v] = o;
+#undef K2_STORE16
 #undef K2_PUT
 #undef K2_PATCH
 #undef K2_BYTE
