@@ -642,6 +642,28 @@ __global__ __launch_bounds__(K3_THREADS) void lzf_parse_rec_kernel(LzfBatch bt, 
                 mode = K3_DECIDE;
             }
         }
+        /* ---- a second candidate test, when it needs no memory: its bitmap
+         * word is in a register or the LDS ring (or it lies in the last
+         * match), and no chain record or byte compare is due ------------- */
+        if (mode == K3_RESOLVE) {
+            const uint32_t qw = q >> 5;
+            const bool in_m = q >= ms;
+            if (in_m || qw == cw || qw >= fl) {
+                const uint32_t word = in_m ? ((q > ms && q + 3u <= me) ? 0u : 0xFFFFFFFFu)
+                                           : qw == cw ? curw : K3_RING(qw);
+                if ((word >> (q & 31u)) & 1u) {                          /* q is the ref */
+                    if (rel != 9u) mode = K3_DECIDE;                     /* else: bytes, next iteration */
+                } else if (reln) {
+                    q = qn;
+                    rel = reln;
+                    reln = 0u;
+                    qn = 0xFFFFFFFFu;
+                } else if (qn != 0xFFFFFFFFu) {                          /* no further link */
+                    rel = 0u;
+                    mode = K3_DECIDE;
+                }
+            }
+        }
         /* ---- literal, or the start of a back-reference --------------------- */
         if (mode == K3_DECIDE) {
             curw |= 1u << (p & 31u);                                     /* p is inserted */
