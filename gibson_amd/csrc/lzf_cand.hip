@@ -423,6 +423,65 @@ __device__ __forceinline__ uint32_t k3_comb(uint32_t rel, uint32_t code)
 
 enum { K3_STEP = 0, K3_RESOLVE = 1, K3_DECIDE = 2, K3_EXTEND = 3, K3_EMIT = 4, K3_DONE = 5 };
 
+/* A value shorter than 16 bytes, whole: the reference's loop
+ * (src/lzf_c.c:145-290) over the bytes in registers, the table replaced by
+ * a search of the inserted positions (at most 13).  Keeps the main loop's
+ * 16-byte loads inside every value. */
+__device__ __noinline__ uint32_t k3_small(const uint8_t *src, uint32_t n, uint8_t *dst, uint32_t cap)
+{
+    const uint4 V = dv_ld16_tail(src, n);
+#define K3S_B(i_) ((dv_sel4(V, (i_) >> 2) >> (8u * ((i_) & 3u))) & 0xFFu)
+#define K3S_SLOT(i_) dv_slot(K3S_B(i_) | (K3S_B((i_) + 1u) << 8) | (K3S_B((i_) + 2u) << 16))
+    uint32_t op = 1u, lit = 0u, ins = 0u, p = 0u;
+    while (p + 2u < n) {                                           /* src/lzf_c.c:145 */
+        const uint32_t s = K3S_SLOT(p);
+        uint32_t q = 0u;
+        for (uint32_t t = p; t-- > 0u;)                            /* the latest inserted, same slot */
+            if (((ins >> t) & 1u) && K3S_SLOT(t) == s) { q = t; break; }
+        ins |= 1u << p;
+        if (q > 0u && p + 4u < n && K3S_B(q) == K3S_B(p) && K3S_B(q + 1u) == K3S_B(p + 1u) &&
+            K3S_B(q + 2u) == K3S_B(p + 2u)) {                      /* src/lzf_c.c:151-158 */
+            const uint32_t maxlen = n - p - 2u;
+            uint32_t len = 3u;
+            while (len < maxlen && K3S_B(q + len) == K3S_B(p + len)) len++;
+            if (op - (lit ? 0u : 1u) + 4u >= cap) return 0u;     /* src/lzf_c.c:172-176 */
+            if (lit) dst[op - lit - 1u] = (uint8_t)(lit - 1u);
+            else op--;
+            const uint32_t off = p - q - 1u, L = len - 2u;
+            if (L < 7u) {
+                dst[op++] = (uint8_t)((off >> 8) | (L << 5));
+            } else {
+                dst[op++] = (uint8_t)((off >> 8) | (7u << 5));
+                dst[op++] = (uint8_t)(L - 7u);
+            }
+            dst[op++] = (uint8_t)off;
+            lit = 0u;
+            op++;
+            p += len;
+            if (p >= n - 2u) break;                                 /* src/lzf_c.c:229 */
+            ins |= (1u << (p - 2u)) | (1u << (p - 1u));
+        } else {
+            if (op >= cap) return 0u;                               /* src/lzf_c.c:263 */
+            lit++;
+            dst[op++] = (uint8_t)K3S_B(p);
+            p++;
+            if (lit == LZF_MAX_LIT) { dst[op - lit - 1u] = (uint8_t)(lit - 1u); lit = 0u; op++; }
+        }
+    }
+    if (op + 3u > cap) return 0u;                                   /* src/lzf_c.c:276 */
+    while (p < n) {                                                 /* src/lzf_c.c:279-288 */
+        lit++;
+        dst[op++] = (uint8_t)K3S_B(p);
+        p++;
+        if (lit == LZF_MAX_LIT) { dst[op - lit - 1u] = (uint8_t)(lit - 1u); lit = 0u; op++; }
+    }
+    if (lit) dst[op - lit - 1u] = (uint8_t)(lit - 1u);
+    else op--;
+    return op;
+#undef K3S_B
+#undef K3S_SLOT
+}
+
 /* The lanes of a wave are at different points of their values, so the loop
  * is a state machine in which every lane does at most ONE unit of each kind
  * of work per iteration -- take the record of p, test one candidate for
@@ -442,6 +501,10 @@ __global__ __launch_bounds__(K3_THREADS) void lzf_parse_rec_kernel(LzfBatch bt, 
     }
     const uint8_t *src = bt.in + bt.in_off[v];
     uint8_t *dst = bt.out + bt.out_off[v];
+    if (n < 16u) {                     /* below one 16-byte window: whole, in registers */
+        bt.out_len[v] = k3_small(src, n, dst, cap);
+        return;
+    }
     const uint32_t *rec = sc.rec + (uint64_t)v * sc.rstride;
     uint32_t *bits = sc.bits + (uint64_t)v * sc.bstride;
 
@@ -540,10 +603,10 @@ __global__ __launch_bounds__(K3_THREADS) void lzf_parse_rec_kernel(LzfBatch bt, 
 #define K3_BYTE(pos_, out_)                                                        \
     do {                                                                           \
         uint32_t d_ = (pos_) - wb;                                                 \
-        if (d_ >= 16u) {                                                           \
-            W = dv_ld16_safe(src + (pos_), n - (pos_));                            \
-            wb = (pos_);                                                           \
-            d_ = 0u;                                                               \
+        if (d_ >= 16u) {                   /* 16 bytes inside the value (n >= 16) */ \
+            wb = dv_at16(n, (pos_));                                               \
+            W = dv_ld16(src + wb);                                                 \
+            d_ = (pos_) - wb;                                                      \
         }                                                                          \
         (out_) = (dv_sel4(W, d_ >> 2) >> (8u * (d_ & 3u))) & 0xFFu;               \
     } while (0)
