@@ -405,7 +405,9 @@ __global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt,
 #ifndef K3_THREADS
 #define K3_THREADS 256u
 #endif
-#define K3_CB      16u          /* records per parse block: 64 bytes of one line */
+#ifndef K3_CB
+#define K3_CB      16u          /* records per parse block: 64 bytes of one line (8: 32 bytes) */
+#endif
 #ifndef K3_RW
 #define K3_RW      32u          /* bitmap words kept in LDS per lane (power of two) */
 #endif
@@ -637,17 +639,23 @@ __global__ __launch_bounds__(K3_THREADS) void lzf_parse_rec_kernel(LzfBatch bt, 
                     const uint4 *cp = (const uint4 *)(rec + cb);
                     C0 = cp[0];
                     C1 = cp[1];
+#if K3_CB == 16
                     C2 = cp[2];
                     C3 = cp[3];
+#endif
                 }
-                /* a select tree over the 16 words (a dynamic index would put
-                 * the block in scratch memory) */
+                /* a select tree over the block's words (a dynamic index would
+                 * put the block in scratch memory) */
                 const bool b0 = d & 1u, b1 = d & 2u;
                 const uint32_t c0 = b1 ? (b0 ? C0.w : C0.z) : (b0 ? C0.y : C0.x);
                 const uint32_t c1 = b1 ? (b0 ? C1.w : C1.z) : (b0 ? C1.y : C1.x);
+#if K3_CB == 16
                 const uint32_t c2 = b1 ? (b0 ? C2.w : C2.z) : (b0 ? C2.y : C2.x);
                 const uint32_t c3 = b1 ? (b0 ? C3.w : C3.z) : (b0 ? C3.y : C3.x);
                 const uint32_t c = (d & 8u) ? ((d & 4u) ? c3 : c2) : ((d & 4u) ? c1 : c0);
+#else
+                const uint32_t c = (d & 4u) ? c1 : c0;
+#endif
                 rel = (c >> 13) & 7u;
                 q = p - 1u - (c & 0x1FFFu);
                 reln = c >> 29;
@@ -805,9 +813,10 @@ __global__ __launch_bounds__(K3_THREADS) void lzf_parse_rec_kernel(LzfBatch bt, 
                     if (nw == cw) {
                         curw |= b1 | b2;
                     } else {
-                        uint32_t wo = curw, wm = 0u, wn = 0u;
-                        if ((t1 >> 5) == cw) wo |= b1; else if ((t1 >> 5) == nw) wn |= b1; else wm |= b1;
-                        if ((t2 >> 5) == cw) wo |= b2; else if ((t2 >> 5) == nw) wn |= b2; else wm |= b2;
+                        const uint32_t w1 = t1 >> 5, w2 = t2 >> 5;
+                        const uint32_t wo = curw | (w1 == cw ? b1 : 0u) | (w2 == cw ? b2 : 0u);
+                        const uint32_t wn = (w1 == nw ? b1 : 0u) | (w2 == nw ? b2 : 0u);
+                        const uint32_t wm = (w1 != cw && w1 != nw ? b1 : 0u) | (w2 != cw && w2 != nw ? b2 : 0u);
                         K3_FLUSH_TO(cw);
                         K3_RING(cw) = wo;
                         /* words cw+1 .. nw-2 are all interior (0), nw-1 holds tails */
