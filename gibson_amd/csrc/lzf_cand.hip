@@ -260,14 +260,17 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 const uint32_t p = B + 64u * j + lane;
                 if (p < np) {
                     c_p = p;
-                    const uint16_t *Ok = O + KT_BLK * (k % 3u), *Op = O + KT_BLK * ((k + 2u) % 3u);
+                    const uint16_t *Ok = O + KT_BLK * (k % 3u);
                     const uint32_t q1 = Ok[64u * j + lane];
                     c_avail = n - p;
                     c_a = ak[(PS + KT_PF - 2u) % KT_PF];              /* A's bytes of block t-2 */
                     if (q1 != 0u && p - q1 <= LZF_WINDOW) {          /* off = p - q - 1 < 8192 */
-                        const uint32_t q2 = q1 >= B ? Ok[q1 - B]
-                                          : q1 + KT_BLK >= B ? Op[q1 + KT_BLK - B]
-                                                             : Q[q1 & (LZF_WINDOW - 1u)];
+                        /* Ok / Op / the ring, as one index into Q..O */
+                        const uint32_t ik = LZF_WINDOW + KT_BLK * (k % 3u), ip = LZF_WINDOW + KT_BLK * ((k + 2u) % 3u);
+                        const uint32_t iq = q1 >= B ? ik + (q1 - B)
+                                          : q1 + KT_BLK >= B ? ip + (q1 + KT_BLK - B)
+                                                             : (q1 & (LZF_WINDOW - 1u));
+                        const uint32_t q2 = Q[iq];
                         c_q1 = l1 = q1;
                         if (q2 != 0u && p - q2 <= LZF_WINDOW) c_q2 = l2 = q2;
                     }
@@ -366,9 +369,11 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
 __global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt, LzfRecScratch sc)
 {
     __shared__ __attribute__((aligned(16))) uint16_t T[LZF_SLOTS + 64u];  /* slot -> latest position, 0: none; + dummies */
-    __shared__ uint16_t Q[LZF_WINDOW];                                 /* q1 of position x at x % 8192 */
+    /* Q: q1 of position x at x % 8192; O (right behind it, one array, so a
+     * q2 lookup is one read at a selected index): q1 of the blocks' positions */
+    __shared__ uint16_t QO[LZF_WINDOW + 3u * KT_BLK];
+    uint16_t *const Q = QO, *const O = QO + LZF_WINDOW;
     __shared__ uint32_t S[2u * KT_BLK];
-    __shared__ uint16_t O[3u * KT_BLK];                                /* q1 of the blocks' positions */
 #if KT_BALLOT
     unsigned long long *const Dw = nullptr;
 #else
