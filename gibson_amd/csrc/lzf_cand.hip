@@ -10,23 +10,22 @@
  * same-slot position q1(p), then q1(q1(p)), ...) that the parse did not skip.
  * Two kernels per batch:
  *
- *   1. lzf_cand_table_kernel -- position-parallel, one value per workgroup
- *      of 8 waves (one per CU: the table is 128 KiB of LDS).  For every
- *      position p: q1(p) and q2(p) = q1(q1(p)), each with how far its bytes
- *      agree with p's (<= 8), packed in a u32 record in HBM scratch.
- *      q1 comes from an exact direct-mapped table T[slot] -> latest position
- *      (65536 x u16, the reference's own table size, src/lzfP.h:55), so
- *      there are no bucket chains to walk on any data; q2 from a ring Q of
- *      q1 over the last 8192 positions (a candidate farther back is outside
- *      every window, src/lzf_c.c:153).  Per block of 512 positions:
- *        A  each wave takes one window of 64 positions: bytes, slot, and the
- *           same-slot lanes of the window (three 64-bit lane bitmaps in LDS,
- *           keyed by the slot's digits; AND of the read-backs is exact);
- *        B  wave w owns the slots with slot % 8 == w and does their table
- *           reads and writes for the whole block, window by window -- one
- *           wave's LDS operations execute in order, so T is read and written
- *           in position order without any cross-wave ordering;
- *        C  each wave takes its window again: q1, q2, agreement, record.
+ *   1. lzf_cand_table_kernel -- position-parallel, one value at a time per
+ *      workgroup of 16 waves (one workgroup per CU: the table is 128 KiB of
+ *      LDS).  For every position p: q1(p) and q2(p) = q1(q1(p)), each with
+ *      how far its bytes agree with p's (<= 8), packed in a u32 record in
+ *      HBM scratch.  q1 comes from an exact direct-mapped table T[slot] ->
+ *      latest position (65536 x u16, the reference's own table size,
+ *      src/lzfP.h:55), so there are no bucket chains to walk on any data; q2
+ *      from a ring Q of q1 over the last 8192 positions (a candidate farther
+ *      back is outside every window, src/lzf_c.c:153).  Blocks of 15
+ *      windows of 64 positions run through a pipeline (kt_value below):
+ *        A  worker wave j takes window j: bytes, slot, and the exact set of
+ *           same-slot lanes of the window (16 ballots of the slot bits);
+ *        B  the table wave does the T reads and writes of the 15 windows in
+ *           order -- one wave's LDS operations execute in order, so T is read
+ *           and written in position order without cross-wave ordering;
+ *        C  each worker takes its window again: q1, q2, agreement, record.
  *
  *   2. lzf_parse_rec_kernel -- the greedy parse and emission, ONE LANE PER
  *      VALUE (a wave advances 64 values at once).  It keeps an inserted-
@@ -51,7 +50,7 @@
 #define RC_LONG 7u
 
 #ifndef KT_WIN
-#define KT_WIN 14u                /* windows of 64 positions per block = worker waves */
+#define KT_WIN 15u                /* windows of 64 positions per block = worker waves: 15 + the table wave = 4 per SIMD */
 #endif
 /* same-slot lanes of a window: from three LDS digit bitmaps per worker
  * (KT_BALLOT 0) or from 16 ballots of the slot's bits (1; no LDS) */
@@ -103,16 +102,17 @@ __device__ __forceinline__ uint32_t kt_agree(uint2 a, const uint8_t *src, uint32
     return k < avail ? k : avail;
 }
 
-/* Pipelined over blocks of KT_BLK = 7 windows (448 positions): wave 0 is the
- * table wave, waves 1..7 are workers, and each step ends with ONE workgroup
- * barrier.  Block k goes through
+/* Pipelined over blocks of KT_BLK = KT_WIN windows (960 positions): wave 0 is
+ * the table wave, waves 1..KT_WIN are workers (16 waves: 4 per SIMD), and
+ * each step ends with ONE workgroup barrier.  Block k goes through
  *   step k    A(k)   worker j: window j -- bytes, slot, same-slot lanes -> S[k%2]
- *   step k+1  B(k)   table wave: T reads/writes of the 7 windows in order -> O[k%3]
+ *   step k+1  B(k)   table wave: T reads/writes of the windows in order -> O[k%3]
  *   step k+2  C1(k)  worker j: q1, q2 (O[k%3], O[(k-1)%3], Q); agreement loads issued
  *   step k+3  C2(k)  worker j: agreement, record stored; Q <- O[k%3]
- * so the agreement loads have a whole step to return.  Q(k) is written in
- * step k+3: the slots it overwrites belong to positions 8192 before block k,
- * which no C1 of block k+1 or later can reach (off < 8192). */
+ * Q(k) is written in step k+3: the slots it overwrites belong to positions
+ * 8192 before block k, which no C1 of block k+1 or later can reach
+ * (off < 8192).  The kernel is VALU-bound: the same-slot
+ * masks cost 4 VALU per slot bit (v_bfe_i32 + ballot + two v_bitop3). */
 /* -DKT_TIMING (diagnostic build): cycles per phase, summed over waves in
  * kt_times[]: [0] table wave B, [1] table wave barrier, [2] C2, [3] C1,
  * [4] A, [5] worker loads, [6] worker barrier, [7] steps */
