@@ -413,6 +413,9 @@ __global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt,
 #ifndef K3_CB
 #define K3_CB      16u          /* records per parse block: 64 bytes of one line (8: 32 bytes) */
 #endif
+#ifndef K3_NRES
+#define K3_NRES    2u           /* candidate tests per loop iteration (2: 206.2 vs 210.8 ms for 1 + a memory-free one) */
+#endif
 #ifndef K3_RW
 #define K3_RW      32u          /* bitmap words kept in LDS per lane (power of two) */
 #endif
@@ -668,73 +671,56 @@ __global__ __launch_bounds__(K3_THREADS) void lzf_parse_rec_kernel(LzfBatch bt, 
                 mode = rel ? K3_RESOLVE : K3_DECIDE;
             }
         }
-        /* ---- is the candidate inserted? else the next chain link ---------- */
-        if (mode == K3_RESOLVE) {
-            K3_CNT(11);
-            uint32_t word;
-            if (q >= ms) {
-                word = (q > ms && q + 3u <= me) ? 0u : 0xFFFFFFFFu;         /* last match's interior */
-            } else {
-                const uint32_t d = cw - (q >> 5);
-                word = d == 0u ? curw : (q >> 5) >= fl ? K3_RING(q >> 5) : bits[q >> 5];
-#ifdef KT_TIMING
-                if (d && (q >> 5) < fl) K3_CNT(12);
-#endif
-            }
-            if ((word >> (q & 31u)) & 1u) {                              /* q is the ref */
-                if (rel == 9u)
-                    rel = (src[q] == src[p] && src[q + 1u] == src[p + 1u] && src[q + 2u] == src[p + 2u]) ? 8u
-                                                                                                        : RC_DIFF;
-                mode = K3_DECIDE;
-            } else if (reln) {                                           /* the record's second link */
-                q = qn;
-                rel = reln;
-                reln = 0u;
-                /* the link after it needs q's own record: mark with reln 0 and
-                 * qn = q (a load below on the next failure) */
-                qn = 0xFFFFFFFFu;
-            } else if (qn == 0xFFFFFFFFu) {                              /* load q's record: two more links */
-                K3_CNT(13);
-                const uint32_t c2 = rec[q];
-                const uint32_t r1 = (c2 >> 13) & 7u, r2 = c2 >> 29;
-                const uint32_t y1 = q - 1u - (c2 & 0x1FFFu), y2 = q - 1u - ((c2 >> 16) & 0x1FFFu);
-                if (!r1 || p - y1 - 1u >= LZF_WINDOW) {                  /* the chain leaves p's window */
-                    rel = 0u;
-                    mode = K3_DECIDE;
+        /* ---- is the candidate inserted? else the next chain link: up to
+         * K3_NRES tests per iteration (a walk past a skipped candidate then
+         * rarely costs the wave an iteration) ------------------------------ */
+#pragma unroll
+        for (uint32_t rt_ = 0; rt_ < K3_NRES; rt_++) {
+            if (mode == K3_RESOLVE) {
+                K3_CNT(11);
+                uint32_t word;
+                if (q >= ms) {
+                    word = (q > ms && q + 3u <= me) ? 0u : 0xFFFFFFFFu;         /* last match's interior */
                 } else {
-                    const uint32_t rq = rel;
-                    rel = k3_comb(rq, r1);
-                    q = y1;
-                    if (r2 && p - y2 - 1u < LZF_WINDOW) {
-                        reln = k3_comb(rq, r2);
-                        qn = y2;
-                    } else {
-                        reln = 0u;
-                        qn = 0u;                                         /* nothing after y1 */
-                    }
+                    const uint32_t d = cw - (q >> 5);
+                    word = d == 0u ? curw : (q >> 5) >= fl ? K3_RING(q >> 5) : bits[q >> 5];
+#ifdef KT_TIMING
+                    if (d && (q >> 5) < fl) K3_CNT(12);
+#endif
                 }
-            } else {                                                     /* no further link */
-                rel = 0u;
-                mode = K3_DECIDE;
-            }
-        }
-        /* ---- a second candidate test, when it needs no memory: its bitmap
-         * word is in a register or the LDS ring (or it lies in the last
-         * match), and no chain record or byte compare is due ------------- */
-        if (mode == K3_RESOLVE) {
-            const uint32_t qw = q >> 5;
-            const bool in_m = q >= ms;
-            if (in_m || qw == cw || qw >= fl) {
-                const uint32_t word = in_m ? ((q > ms && q + 3u <= me) ? 0u : 0xFFFFFFFFu)
-                                           : qw == cw ? curw : K3_RING(qw);
-                if ((word >> (q & 31u)) & 1u) {                          /* q is the ref */
-                    if (rel != 9u) mode = K3_DECIDE;                     /* else: bytes, next iteration */
-                } else if (reln) {
+                if ((word >> (q & 31u)) & 1u) {                              /* q is the ref */
+                    if (rel == 9u)
+                        rel = (src[q] == src[p] && src[q + 1u] == src[p + 1u] && src[q + 2u] == src[p + 2u]) ? 8u
+                                                                                                            : RC_DIFF;
+                    mode = K3_DECIDE;
+                } else if (reln) {                                           /* the record's second link */
                     q = qn;
                     rel = reln;
                     reln = 0u;
+                    /* the link after it needs q's own record: mark with reln 0 and
+                     * qn = q (a load below on the next failure) */
                     qn = 0xFFFFFFFFu;
-                } else if (qn != 0xFFFFFFFFu) {                          /* no further link */
+                } else if (qn == 0xFFFFFFFFu) {                              /* load q's record: two more links */
+                    K3_CNT(13);
+                    const uint32_t c2 = rec[q];
+                    const uint32_t r1 = (c2 >> 13) & 7u, r2 = c2 >> 29;
+                    const uint32_t y1 = q - 1u - (c2 & 0x1FFFu), y2 = q - 1u - ((c2 >> 16) & 0x1FFFu);
+                    if (!r1 || p - y1 - 1u >= LZF_WINDOW) {                  /* the chain leaves p's window */
+                        rel = 0u;
+                        mode = K3_DECIDE;
+                    } else {
+                        const uint32_t rq = rel;
+                        rel = k3_comb(rq, r1);
+                        q = y1;
+                        if (r2 && p - y2 - 1u < LZF_WINDOW) {
+                            reln = k3_comb(rq, r2);
+                            qn = y2;
+                        } else {
+                            reln = 0u;
+                            qn = 0u;                                         /* nothing after y1 */
+                        }
+                    }
+                } else {                                                     /* no further link */
                     rel = 0u;
                     mode = K3_DECIDE;
                 }
@@ -836,6 +822,12 @@ __global__ __launch_bounds__(K3_THREADS) void lzf_parse_rec_kernel(LzfBatch bt, 
                 }
             }
         }
+#ifdef KT_ENDMODE   /* diagnostics: lanes that end an iteration mid-step, by mode */
+        k3c[4] += mode == K3_RESOLVE;
+        k3c[5] += mode == K3_DECIDE;
+        k3c[6] += mode == K3_EXTEND;
+        k3c[7] += mode == K3_EMIT;
+#endif
     }
 #ifdef KT_TIMING
     k3c[1] = __builtin_amdgcn_s_memtime() - k3t0;
