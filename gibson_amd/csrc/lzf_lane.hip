@@ -913,6 +913,9 @@ extern "C" int lzf_gpu_debug_sites(unsigned long long *out16, int reset)
  * insertion (or hop one link back), compare one 16-byte piece of a long
  * match, emit one literal or one back-reference -- and a long walk or match
  * of one lane costs the others only the small blocks it runs through. */
+#ifndef K2_NRES
+#define K2_NRES 1u
+#endif
 enum { K2_STEP = 0, K2_RESOLVE = 1, K2_DECIDE = 2, K2_EXTEND = 3, K2_EMIT = 4, K2_DONE = 5 };
 
 __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt, LzfLaneScratch sc)
@@ -1072,33 +1075,37 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                 mode = rel ? K2_RESOLVE : K2_DECIDE;
             }
         }
-        /* ---- is the candidate inserted? else one link back --------------- */
-        if (mode == K2_RESOLVE) {
-            uint32_t word;
-            if (q >= ms) {
-                word = (q > ms && q + 3u <= me) ? 0u : 0xFFFFFFFFu;         /* last match's interior */
-            } else {
-                const uint32_t d = cw - (q >> 5);
-                if (d != 0u && (q >> 5) < fl) K2_SITE(3);
-                word = d == 0u ? curw : (q >> 5) >= fl ? K2_RING(q >> 5) : bits[q >> 5];
-            }
-            if ((word >> (q & 31u)) & 1u) {                              /* q is the ref */
-                if (rel == 9u) K2_SITE(5);
-                if (rel == 9u)
-                    rel = (src[q] == src[p] && src[q + 1u] == src[p + 1u] && src[q + 2u] == src[p + 2u]) ? 8u : 1u;
-                mode = K2_DECIDE;
-            } else {
-                K2_SITE(4);
-                const uint32_t c2 = cand[q];
-                const uint32_t r2 = c2 >> 13;
-                const uint32_t q2 = q - 1u - (c2 & 0x1FFFu);
-                if (!r2 || p - q2 - 1u >= LZF_WINDOW) {
-                    rel = 0u;
+        /* ---- is the candidate inserted? else one link back: up to K2_NRES
+         * tests per iteration ---------------------------------------------- */
+#pragma unroll
+        for (uint32_t rt_ = 0; rt_ < K2_NRES; rt_++) {
+            if (mode == K2_RESOLVE) {
+                uint32_t word;
+                if (q >= ms) {
+                    word = (q > ms && q + 3u <= me) ? 0u : 0xFFFFFFFFu;         /* last match's interior */
+                } else {
+                    const uint32_t d = cw - (q >> 5);
+                    if (d != 0u && (q >> 5) < fl) K2_SITE(3);
+                    word = d == 0u ? curw : (q >> 5) >= fl ? K2_RING(q >> 5) : bits[q >> 5];
+                }
+                if ((word >> (q & 31u)) & 1u) {                              /* q is the ref */
+                    if (rel == 9u) K2_SITE(5);
+                    if (rel == 9u)
+                        rel = (src[q] == src[p] && src[q + 1u] == src[p + 1u] && src[q + 2u] == src[p + 2u]) ? 8u : 1u;
                     mode = K2_DECIDE;
                 } else {
-                    const bool e1 = rel >= 2u && rel <= 8u, e2 = r2 >= 2u;
-                    rel = rel == 9u ? 9u : (e1 && e2) ? 8u : (e1 != e2) ? 1u : 9u;
-                    q = q2;
+                    K2_SITE(4);
+                    const uint32_t c2 = cand[q];
+                    const uint32_t r2 = c2 >> 13;
+                    const uint32_t q2 = q - 1u - (c2 & 0x1FFFu);
+                    if (!r2 || p - q2 - 1u >= LZF_WINDOW) {
+                        rel = 0u;
+                        mode = K2_DECIDE;
+                    } else {
+                        const bool e1 = rel >= 2u && rel <= 8u, e2 = r2 >= 2u;
+                        rel = rel == 9u ? 9u : (e1 && e2) ? 8u : (e1 != e2) ? 1u : 9u;
+                        q = q2;
+                    }
                 }
             }
         }
