@@ -500,7 +500,10 @@ __device__ __noinline__ uint32_t k3_small(const uint8_t *src, uint32_t n, uint8_
  * instruction touches one line per lane (64 values), so the kernel is shaped
  * to issue few of them: records in 64-byte blocks, output in 16-byte stores,
  * the input in 16-byte windows, the bitmap's recent words in LDS. */
-__global__ __launch_bounds__(K3_THREADS) void lzf_parse_rec_kernel(LzfBatch bt, LzfRecScratch sc)
+#ifndef K3_MINB
+#define K3_MINB 1
+#endif
+__global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfBatch bt, LzfRecScratch sc)
 {
     const uint32_t v = blockIdx.x * K3_THREADS + threadIdx.x;
     if (v >= bt.count) return;
