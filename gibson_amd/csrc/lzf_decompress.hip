@@ -1,15 +1,15 @@
 /*
  * lzf_decompress.hip -- token-parallel LZF decoder for gfx950.
  *
- * Replaces src/lzf_d.c:55-149 for batches of independent streams: one
- * workgroup = one 64-lane wave per stream.  The stream is consumed in
- * rounds; a round starts at a token boundary and covers the tokens that
- * START in the next 128 input bytes (CD_ROUND):
+ * Replaces src/lzf_d.c:55-149 for batches of independent streams.  A stream
+ * is consumed in rounds; a round starts at a token boundary and covers the
+ * tokens that START in the next 128 input bytes (CD_ROUND):
  *
- *   1. token boundaries: every lane takes two input bytes and their token
- *      sizes (literal c<32: c+2 bytes; back-ref: 2, or 3 when c>>5 == 7);
- *      the chain of boundaries is found by pointer doubling (ds_bpermute),
- *      and lane l ends up holding the start of token l (<= 64 per round);
+ *   1. token boundaries: every lane sizes the tokens that would start at its
+ *      two positions of the round (literal c<32: c+2 bytes; back-ref: 2, or 3
+ *      when c>>5 == 7); the chain of boundaries is found by pointer doubling
+ *      (ds_bpermute) or by a scalar walk over runs of 2-byte tokens, and lane
+ *      l ends up holding the start of token l (<= 64 per round);
  *   2. lane l decodes token l (src/lzf_d.c:66-119) and the output offsets
  *      follow from one wave prefix sum (DPP) of the token output lengths;
  *   3. the reference's error checks, in its order (literal: E2BIG then
@@ -23,30 +23,44 @@
  *      src/lzf_d.c:137-142 copies byte-serially so overlap replicates) is
  *      resolved by pointer doubling over the group's lanes.  Every group is
  *      stored to HBM as it completes.
+ *
+ * Steps 1-3 depend on the input alone, step 4 on the output of the rounds
+ * before.  Each wave's round is a chain of dependent LDS round trips, and a
+ * stream's LDS (the 8 KiB output window) allows ~4 streams per SIMD, so one
+ * wave per stream leaves the SIMDs waiting on LDS latency.  `pipe` (the
+ * product form) gives a stream two waves: a producer runs steps 1-3 one round
+ * ahead and hands the round's token table over in LDS (double-buffered, one
+ * workgroup barrier per round); a consumer runs step 4.  `tokpar64` (one wave
+ * does everything) stays as the single-wave form.
  */
 #include "lzf_internal.h"
 
 #define CD_LANES   64u
-#ifndef CD_ROUND
-#define CD_ROUND   128              /* input bytes whose token starts one round covers: 64 or 128 */
-#endif
+#define CD_ROUND   128u             /* input bytes whose token starts one round covers */
 /* input ring: a round reads [base, base + CD_ROUND + 33); staging runs in
  * CD_STAGE-byte pieces (one 16-byte load per lane) when the round's reach
  * passes base + 2 * CD_ROUND (loaded < base + 2 * CD_ROUND), so a piece
- * overwrites only bytes before loaded - CD_IN_RING + CD_STAGE < base, which
- * no later round reads.  A small ring keeps the kernel's LDS small:
- * residency, not bandwidth, bounds this decoder */
-#ifndef CD_IN_RING
-#define CD_IN_RING 512u
-#endif
-#define CD_STAGE   (CD_IN_RING / 2u)
-static_assert(CD_STAGE >= 2u * CD_ROUND && CD_STAGE <= 16u * CD_LANES, "one staging piece per round");
+ * overwrites only bytes before loaded - in_ring + CD_STAGE.  Single wave:
+ * ring 512, piece 256, which is < base.  Pipe: the consumer still reads
+ * round k's literals, [base_k, base_k + 161), while the producer stages for
+ * round k + 1 (base_{k+1} <= base_k + 160): ring 1024, piece 512, so a piece
+ * overwrites only bytes before base_{k+1} - 256 < base_k */
+#define CD_IN_RING1 512u
+#define CD_IN_RING2 1024u
 /* output window ring: back-references reach at most 8192 bytes back
  * (src/lzf_d.c:95, off < 8192), and a group reads all its sources before it
  * writes its 64 bytes, so a ring of 8 KiB suffices: the slots a group
  * overwrites (o - 8192) are read, if at all, by that group alone */
 #ifndef CD_OUT_MAX
 #define CD_OUT_MAX 8192u
+#endif
+/* token discovery: 1 = the scalar walk over size-2 runs, 0 = pointer doubling */
+#ifndef CD_WALK
+#define CD_WALK    0
+#endif
+/* decoder form: 1 = pipe (producer + consumer wave per stream), 0 = tokpar64 */
+#ifndef CD_PIPE
+#define CD_PIPE    1
 #endif
 
 /* 16 bytes from p, of which `avail` (< 16: the rest reads as zero) exist */
@@ -62,15 +76,38 @@ __device__ __forceinline__ uint4 cd_ld16(const uint8_t *p, uint32_t avail)
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-__device__ __forceinline__ uint64_t cd_lt(uint32_t i)
-{
-    return i >= 64u ? ~0ull : ((1ull << i) - 1ull);
-}
-
 __device__ __forceinline__ void cd_fence()
 {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+}
+
+#ifdef CD_TIMING
+/* diagnostic build: per role, cycles working and cycles waiting at the
+ * pipe's barriers, summed over waves (lzf_gpu_dec_tstat) */
+__device__ unsigned long long cd_tstat[8];
+#endif
+
+/* workgroup barrier with LDS release/acquire (the pipe's hand-over); tw[0]
+ * accumulates working cycles, tw[1] waiting ones (CD_TIMING builds) */
+__device__ __forceinline__ void cd_barrier(uint64_t *tw = nullptr)
+{
+#ifdef CD_TIMING
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#ifdef CD_TIMING
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    if (tw) {
+        tw[0] += t0 - tw[2];
+        tw[1] += t1 - t0;
+        tw[2] = t1;
+    }
+#else
+    (void)tw;
+#endif
 }
 
 __device__ __forceinline__ uint32_t cd_incl_sum(uint32_t x)
@@ -84,231 +121,287 @@ __device__ __forceinline__ uint32_t cd_incl_sum(uint32_t x)
     return x;
 }
 
-__device__ __forceinline__ uint32_t cd_incl_max(uint32_t x)
-{
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false));
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false));
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false));
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false));
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
-    return x;
-}
-
-/* J(J(i)) for a jump table J whose exits are CD_LANES (= stay) */
-__device__ __forceinline__ uint32_t cd_jump(uint32_t j)
-{
-    const uint32_t t = (uint32_t)__shfl((int)j, (int)(j & 63u));
-    return j >= 64u ? 64u : t;
-}
-
 __device__ __forceinline__ uint32_t cd_rl(uint32_t v, uint32_t l)
 {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
 
+__device__ __forceinline__ uint32_t cd_tsz(uint32_t c)
+{
+    return c < 32u ? c + 2u : ((c >> 5) == 7u ? 3u : 2u);
+}
+
+/* stage input [base, base + 2 * CD_ROUND) (tokens starting in the round and
+ * their literal payloads, <= CD_ROUND - 1 + 33 bytes) into the input ring */
+template <uint32_t IN_RING>
+__device__ __forceinline__ void cd_stage(uint8_t *inr, const uint8_t *src, uint32_t base, uint32_t avail,
+                                         uint32_t &loaded, uint32_t lane)
+{
+    constexpr uint32_t STAGE = IN_RING / 2u;
+    static_assert(STAGE >= 2u * CD_ROUND && STAGE <= 16u * CD_LANES, "one staging piece per round");
+    uint32_t need = base + 2u * CD_ROUND;
+    if (need > avail) need = avail;
+    if (loaded < need) {                 /* need - loaded <= CD_ROUND + 33 <= STAGE */
+        uint32_t to = loaded + STAGE;
+        if (to > avail) to = avail;
+        const uint32_t x = loaded + 16u * lane;   /* loaded is a multiple of 16 here */
+        if (x < to) *(uint4 *)(inr + (x & (IN_RING - 1u))) = cd_ld16(src + x, to - x);
+        loaded = to;
+        cd_fence();
+    }
+}
+
+/* step 1: lane l gets the round-relative start of token l (CD_ROUND: none);
+ * nbase = the input offset after the round's last token */
+__device__ __forceinline__ uint32_t cd_discover(const uint8_t *inr, uint32_t imask, uint8_t *tokpos,
+                                                uint32_t base, uint32_t in_len, uint32_t lane, uint32_t &nbase)
+{
+    const uint32_t pa = 2u * lane, pb = pa + 1u;
+    const uint32_t ca = inr[(base + pa) & imask], cb = inr[(base + pb) & imask];
+    const uint32_t ta = cd_tsz(ca), tb = cd_tsz(cb);
+#if CD_WALK
+    /* a scalar walk: the 2-byte back-references (the bulk of a stream) become
+     * two lane masks, one per parity, so a run of them is skipped in one step
+     * and only literals and 3-byte back-references are stepped over one by
+     * one.  Tokens start at the walk's positions below lim; the first token
+     * is decoded even from an empty stream (src/lzf_d.c:64 is a do-while) */
+    uint32_t lim = in_len > base ? in_len - base : 0u;
+    if (lim > CD_ROUND) lim = CD_ROUND;
+    if (lim == 0u) lim = 1u;
+    const uint64_t E2 = __ballot(ta == 2u && pa < lim);
+    const uint64_t O2 = __ballot(tb == 2u && pb < lim);
+    const uint32_t tsz2 = ta | (tb << 8);
+    uint64_t SE = 0ull, SO = 0ull;
+    uint32_t pos = 0;
+    /* one branch per parity keeps the masks out of selects; a run from bit j
+     * of mask m is the bits below the lowest clear bit of y = m >> j */
+    for (;;) {
+        const uint32_t j = pos >> 1;
+        if (pos & 1u) {
+            const uint64_t y = O2 >> j;
+            const uint64_t run = (~y & (y + 1ull)) - 1ull;
+            SO |= run << j;
+            pos += 2u * (uint32_t)__builtin_popcountll(run);
+            if (pos >= lim) break;
+            SO |= 1ull << (pos >> 1);
+            pos += cd_rl(tsz2, pos >> 1) >> 8;
+        } else {
+            const uint64_t y = E2 >> j;
+            const uint64_t run = (~y & (y + 1ull)) - 1ull;
+            SE |= run << j;
+            pos += 2u * (uint32_t)__builtin_popcountll(run);
+            if (pos >= lim) break;
+            SE |= 1ull << (pos >> 1);
+            pos += cd_rl(tsz2, pos >> 1) & 0xFFu;
+        }
+        if (pos >= lim) break;
+    }
+    nbase = base + pos;
+    /* lane l takes the l-th start: ranks by mbcnt, scattered through LDS */
+    const bool sa = (SE >> lane) & 1ull, sb = (SO >> lane) & 1ull;
+    const uint32_t ra = __builtin_amdgcn_mbcnt_hi((uint32_t)(SE >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)SE, 0u)) +
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(SO >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)SO, 0u));
+    if (sa) tokpos[ra] = (uint8_t)pa;
+    if (sb) tokpos[ra + (sa ? 1u : 0u)] = (uint8_t)pb;
+    cd_fence();
+    const uint32_t nt = (uint32_t)__builtin_popcountll(SE) + (uint32_t)__builtin_popcountll(SO);
+    return lane < nt ? tokpos[lane] : CD_ROUND;
+#else
+    (void)tokpos;
+    /* jump tables J0..J5 over the round's 128 positions packed two per lane
+     * (16 bits each; 128 = leaves the round).  A round holds <= 64 tokens
+     * (each takes >= 2 bytes): lane l finds the start of token l with six
+     * doubling levels */
+    uint32_t PJ[6];
+    {
+        const uint32_t ipa = base + pa, ipb = ipa + 1u;
+        uint32_t na = pa + ta, nb = pb + tb;
+        if (ipa + ta >= in_len || na > CD_ROUND) na = CD_ROUND;
+        if (ipb + tb >= in_len || nb > CD_ROUND) nb = CD_ROUND;
+        PJ[0] = na | (nb << 16);
+    }
+#pragma unroll
+    for (uint32_t k = 1; k < 6u; k++) {
+        const uint32_t ja = PJ[k - 1u] & 0xFFFFu, jb = PJ[k - 1u] >> 16;
+        const uint32_t wa = (uint32_t)__shfl((int)PJ[k - 1u], (int)((ja >> 1) & 63u));
+        const uint32_t wb = (uint32_t)__shfl((int)PJ[k - 1u], (int)((jb >> 1) & 63u));
+        const uint32_t va = ja >= CD_ROUND ? CD_ROUND : ((ja & 1u) ? wa >> 16 : wa & 0xFFFFu);
+        const uint32_t vb = jb >= CD_ROUND ? CD_ROUND : ((jb & 1u) ? wb >> 16 : wb & 0xFFFFu);
+        PJ[k] = va | (vb << 16);
+    }
+    uint32_t x = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 6u; b++) {
+        const uint32_t w = (uint32_t)__shfl((int)PJ[b], (int)((x >> 1) & 63u));
+        const uint32_t y = (x & 1u) ? w >> 16 : w & 0xFFFFu;
+        if (((lane >> b) & 1u) && x < CD_ROUND) x = y;
+    }
+    /* the next round starts after the last token */
+    const bool tok = x < CD_ROUND;
+    const uint32_t ntok = (uint32_t)__builtin_popcountll(__ballot(tok));
+    const uint32_t c = inr[(base + (tok ? x : 0u)) & imask];
+    nbase = base + cd_rl(x + cd_tsz(c), ntok - 1u);
+    return x;
+#endif
+}
+
+/* steps 2-3 for lane l's token: its output offset within the round (rel),
+ * the owner info of its output bytes (tinfo: literal -> input ring index
+ * o + tinfo, flagged in bit 31; back-ref -> distance), the round's output
+ * bytes, and errno of the first failing token (0: none) */
+struct CdRound {
+    uint32_t rel, tinfo, total;
+    int32_t err;
+};
+
+__device__ __forceinline__ CdRound cd_decode(const uint8_t *inr, uint32_t imask, uint32_t base, uint32_t x,
+                                             uint32_t O, uint32_t in_len, uint32_t cap)
+{
+    const bool tok = x < CD_ROUND;
+    const uint32_t ip = base + (tok ? x : 0u);
+    const uint32_t c = inr[ip & imask];
+    const uint32_t b1 = inr[(ip + 1u) & imask], b2 = inr[(ip + 2u) & imask];
+    const bool lit = c < 32u;
+    uint32_t olen, back = 0, lsrc = 0;
+    if (lit) {
+        olen = c + 1u;
+        lsrc = ip + 1u;
+    } else {
+        uint32_t len = c >> 5, offb = b1;
+        if (len == 7u) { len += b1; offb = b2; }
+        olen = len + 2u;
+        back = ((c & 31u) << 8) + offb + 1u;
+    }
+    const uint32_t ol = tok ? olen : 0u;
+    const uint32_t incl = cd_incl_sum(ol);
+    CdRound r;
+    r.rel = incl - ol;
+    const uint32_t Ot = O + r.rel;                      /* output offset of my token */
+    r.tinfo = lit ? (((lsrc - Ot) & 0x7FFFFFFFu) | 0x80000000u) : back;
+    r.total = cd_rl(incl, 63u);
+    /* away from the stream's end (every token byte of the round, at most
+     * base + CD_ROUND + 32, lies inside the input) and with the round's output
+     * inside the cap, only a back-reference before the output start can fail */
+    int32_t e = 0;
+    if (base + CD_ROUND + 33u <= in_len && (uint64_t)O + r.total <= cap) {
+        if (tok && !lit && back > Ot) e = 22;                               /* :127 */
+    } else if (tok) {
+        if (lit) {
+            if ((uint64_t)Ot + olen > cap) e = 7;                           /* E2BIG  :72 */
+            else if ((uint64_t)ip + 1u + olen > in_len) e = 22;             /* EINVAL :79 */
+        } else {
+            if (ip + 1u >= in_len) e = 22;                                  /* :101 */
+            else if ((c >> 5) == 7u && ip + 2u >= in_len) e = 22;          /* :111 */
+            else if ((uint64_t)Ot + olen > cap) e = 7;                      /* :121 */
+            else if (back > Ot) e = 22;                                     /* :127 */
+        }
+    }
+    const uint64_t EB = __ballot(e != 0);
+    r.err = EB ? (int32_t)cd_rl((uint32_t)e, (uint32_t)__builtin_ctzll(EB)) : 0;
+    return r;
+}
+
+/* step 4: the round's output [O, O + total), 64 bytes per step.  Tokens sit
+ * in lanes in output order, so the owner of output byte b of a group is
+ * (tokens started before the group) + (token starts in the group at or below
+ * b) - 1: the starts are marked in LDS with the group's tag (gb + 1, never
+ * reused, so the marks need no clearing) and read back as one ballot */
+template <uint32_t IN_RING>
+__device__ __forceinline__ void cd_output(const uint8_t *inr, uint8_t *outr, uint32_t omask, uint32_t *mark,
+                                          uint8_t *dst, uint32_t O, uint32_t total, bool tok, uint32_t Ot,
+                                          uint32_t tinfo, uint32_t lane)
+{
+    constexpr uint32_t imask = IN_RING - 1u;
+    uint32_t tbase = 0;          /* tokens started before the group */
+#ifdef LZF_CD_ABLATE_OUTPUT           /* diagnostic builds only: time discovery alone */
+    total = 0u;
+#endif
+    for (uint32_t g = 0; g < total; g += CD_LANES) {
+        const uint32_t gb = O + g;                     /* group's first output offset */
+        if (tok && Ot >= gb && Ot < gb + CD_LANES) mark[Ot - gb] = gb + 1u;
+        cd_fence();
+        const uint64_t S = __ballot(mark[lane] == gb + 1u);
+        const uint32_t le = __builtin_amdgcn_mbcnt_hi((uint32_t)(S >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)S, 0u)) +
+                            (uint32_t)((S >> lane) & 1ull);
+        const uint32_t k = tbase + le - 1u;
+        tbase += (uint32_t)__builtin_popcountll(S);
+        const uint32_t o = gb + lane;
+        const bool live = g + lane < total;
+        const uint32_t tInf = (uint32_t)__shfl((int)tinfo, (int)k);
+        uint32_t val = 0;
+        int ptr = -1;
+        if (live) {
+            if (tInf >> 31) {
+                val = inr[(o + tInf) & imask];
+            } else {
+                const uint32_t so = o - tInf;
+                if (so >= gb) ptr = (int)(so - gb);
+                else val = outr[so & omask];
+            }
+        }
+        /* in-group back-references (runs): pointer doubling */
+        while (__ballot(ptr >= 0)) {
+            const int pi = ptr >= 0 ? ptr : (int)lane;
+            const uint32_t pv = (uint32_t)__shfl((int)val, pi);
+            const int pp = __shfl(ptr, pi);
+            if (ptr >= 0) { val = pv; ptr = pp; }
+        }
+        if (live) {
+            outr[o & omask] = (uint8_t)val;
+            dst[o] = (uint8_t)val;
+        }
+        cd_fence();
+    }
+}
+
+/* a value past the batch's stated max_out_cap is refused, never overrun */
+__device__ __forceinline__ bool cd_refused(const LzfBatch &bt, uint32_t v, uint32_t lane)
+{
+    if (bt.out_cap[v] <= bt.max_len) return false;
+    if (lane == 0) {
+        bt.out_len[v] = 0u;
+        bt.err[v] = 22;             /* EINVAL */
+    }
+    return true;
+}
+
 __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, uint32_t out_ring)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t *inr = smem;                               /* CD_IN_RING */
-    uint8_t *outr = smem + CD_IN_RING;                 /* out_ring (power of two) */
+    uint8_t *inr = smem;                               /* CD_IN_RING1 */
+    uint8_t *outr = smem + CD_IN_RING1;                /* out_ring (power of two) */
     uint32_t *mark = (uint32_t *)(outr + out_ring);    /* 64 token-start marks (group tags) */
-    const uint32_t imask = CD_IN_RING - 1u, omask = out_ring - 1u;
+    uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* the walk's token starts, in order */
+    const uint32_t imask = CD_IN_RING1 - 1u, omask = out_ring - 1u;
 
     const uint32_t lane = threadIdx.x;
     const uint32_t v = blockIdx.x;
-    if (bt.skip && bt.skip[v]) return;
+    if ((bt.skip && bt.skip[v]) || cd_refused(bt, v, lane)) return;
     const uint32_t in_len = bt.in_len[v];
     const uint32_t cap = bt.out_cap[v];
     const uint8_t *src = bt.in + bt.in_off[v];
     uint8_t *dst = bt.out + bt.out_off[v];
-    if (cap > bt.max_len) {          /* past the batch's stated max_out_cap: refused, never overrun */
-        if (lane == 0) {
-            bt.out_len[v] = 0u;
-            bt.err[v] = 22;         /* EINVAL */
-        }
-        return;
-    }
     /* as the reference, a 0-length stream still reads its first control byte */
     const uint32_t avail = in_len ? in_len : 1u;
 
     mark[lane] = 0u;            /* group tags are >= 1 */
-    uint32_t loaded = 0;
-    uint32_t base = 0;          /* input offset of the round's first token */
-    uint32_t O = 0;             /* output bytes produced so far */
+    uint32_t loaded = 0, base = 0, O = 0;
     int32_t err = 0;
     bool first = true;
-
     while (first || base < in_len) {                     /* src/lzf_d.c:64, 146 */
         first = false;
-        /* stage input [base, base + 2 * CD_ROUND) (tokens starting in the
-         * round and their literal payloads, <= CD_ROUND - 1 + 33 bytes) */
-        uint32_t need = base + 2u * CD_ROUND;
-        if (need > avail) need = avail;
-        if (loaded < need) {                 /* need - loaded <= CD_ROUND + 33 <= CD_STAGE */
-            uint32_t to = loaded + CD_STAGE;
-            if (to > avail) to = avail;
-            const uint32_t x = loaded + 16u * lane;   /* loaded is a multiple of 16 here */
-            if (x < to) *(uint4 *)(inr + (x & imask)) = cd_ld16(src + x, to - x);
-            loaded = to;
-            cd_fence();
-        }
-
-        /* ---- 1. token boundaries -------------------------------------- */
-#if CD_ROUND == 128
-        /* two input bytes per lane; jump tables J0..J5 over the round's 128
-         * positions packed two per lane (16 bits each; 128 = leaves the round).
-         * A round holds <= 64 tokens (each takes >= 2 bytes): lane l finds the
-         * start of token l with six doubling levels */
-        uint32_t PJ[6];
-        {
-            const uint32_t ipa = base + 2u * lane, ipb = ipa + 1u;
-            const uint32_t ca = inr[ipa & imask], cb = inr[ipb & imask];
-            const uint32_t ta = ca < 32u ? ca + 2u : ((ca >> 5) == 7u ? 3u : 2u);
-            const uint32_t tb = cb < 32u ? cb + 2u : ((cb >> 5) == 7u ? 3u : 2u);
-            uint32_t na = 2u * lane + ta, nb = 2u * lane + 1u + tb;
-            if (ipa + ta >= in_len || na > 128u) na = 128u;
-            if (ipb + tb >= in_len || nb > 128u) nb = 128u;
-            PJ[0] = na | (nb << 16);
-        }
-#pragma unroll
-        for (uint32_t k = 1; k < 6u; k++) {
-            const uint32_t ja = PJ[k - 1u] & 0xFFFFu, jb = PJ[k - 1u] >> 16;
-            const uint32_t wa = (uint32_t)__shfl((int)PJ[k - 1u], (int)((ja >> 1) & 63u));
-            const uint32_t wb = (uint32_t)__shfl((int)PJ[k - 1u], (int)((jb >> 1) & 63u));
-            const uint32_t va = ja >= 128u ? 128u : ((ja & 1u) ? wa >> 16 : wa & 0xFFFFu);
-            const uint32_t vb = jb >= 128u ? 128u : ((jb & 1u) ? wb >> 16 : wb & 0xFFFFu);
-            PJ[k] = va | (vb << 16);
-        }
-        uint32_t x = 0;
-#pragma unroll
-        for (uint32_t b = 0; b < 6u; b++) {
-            const uint32_t w = (uint32_t)__shfl((int)PJ[b], (int)((x >> 1) & 63u));
-            const uint32_t y = (x & 1u) ? w >> 16 : w & 0xFFFFu;
-            if (((lane >> b) & 1u) && x < 128u) x = y;
-        }
-        /* lane l now holds token l (tokens compacted in order): its bytes */
-        const bool tok = x < 128u;
-#else
-        const uint32_t ip0 = base + lane;
-        const uint32_t c0 = inr[ip0 & imask];
-        const uint32_t tsz0 = c0 < 32u ? c0 + 2u : ((c0 >> 5) == 7u ? 3u : 2u);
-        uint32_t nx = lane + tsz0;
-        if (ip0 + tsz0 >= in_len || nx > CD_LANES) nx = CD_LANES;  /* loop ends / next round */
-        /* every token takes >= 2 input bytes, so a round has <= 32 tokens:
-         * lane l < 32 finds the start of token l with 5 doubling levels */
-        /* every lane takes part in every shuffle: a shuffle under a partial
-         * exec mask reads nothing from the inactive source lanes */
-        uint32_t J0 = nx, J1, J2, J3, J4;
-        J1 = cd_jump(J0);
-        J2 = cd_jump(J1);
-        J3 = cd_jump(J2);
-        J4 = cd_jump(J3);
-        uint32_t x = 0, y;
-        y = (uint32_t)__shfl((int)J0, (int)(x & 63u)); if ((lane & 1u) && x < CD_LANES) x = y;
-        y = (uint32_t)__shfl((int)J1, (int)(x & 63u)); if ((lane & 2u) && x < CD_LANES) x = y;
-        y = (uint32_t)__shfl((int)J2, (int)(x & 63u)); if ((lane & 4u) && x < CD_LANES) x = y;
-        y = (uint32_t)__shfl((int)J3, (int)(x & 63u)); if ((lane & 8u) && x < CD_LANES) x = y;
-        y = (uint32_t)__shfl((int)J4, (int)(x & 63u)); if ((lane & 16u) && x < CD_LANES) x = y;
-        if (lane >= 32u) x = CD_LANES;
-        /* lane l now holds token l (tokens compacted in order): its bytes */
-        const bool tok = x < CD_LANES;
-#endif
-        const uint32_t ntok = (uint32_t)__builtin_popcountll(__ballot(tok));
-        const uint32_t ip = base + (tok ? x : 0u);
-        const uint32_t c = inr[ip & imask];
-        const uint32_t b1 = inr[(ip + 1u) & imask], b2 = inr[(ip + 2u) & imask];
-        const uint32_t tsz = c < 32u ? c + 2u : ((c >> 5) == 7u ? 3u : 2u);
-
-        /* ---- 2. decode + output offsets ------------------------------- */
-        const bool lit = c < 32u;
-        uint32_t olen, back = 0, lsrc = 0;
-        int32_t e = 0;
-        if (lit) {
-            olen = c + 1u;
-            lsrc = ip + 1u;
-        } else {
-            uint32_t len = c >> 5, offb = b1;
-            if (len == 7u) { len += b1; offb = b2; }
-            olen = len + 2u;
-            back = ((c & 31u) << 8) + offb + 1u;
-        }
-        /* the owner's info for an output byte o: literal -> input ring index
-         * o + (lsrc - Ot), flagged in bit 31; back-ref -> distance */
-        const uint32_t ol = tok ? olen : 0u;
-        const uint32_t incl = cd_incl_sum(ol);
-        const uint32_t Ot = O + incl - ol;                 /* output offset of my token */
-        const uint32_t tinfo = lit ? (((lsrc - Ot) & 0x7FFFFFFFu) | 0x80000000u) : back;
-        /* ---- 3. the reference's checks, in its order ------------------ */
-        if (tok) {
-            if (lit) {
-                if ((uint64_t)Ot + olen > cap) e = 7;                       /* E2BIG  :72 */
-                else if ((uint64_t)ip + 1u + olen > in_len) e = 22;         /* EINVAL :79 */
-            } else {
-                if (ip + 1u >= in_len) e = 22;                              /* :101 */
-                else if ((c >> 5) == 7u && ip + 2u >= in_len) e = 22;      /* :111 */
-                else if ((uint64_t)Ot + olen > cap) e = 7;                  /* :121 */
-                else if (back > Ot) e = 22;                                 /* :127 */
-            }
-        }
-        const uint64_t EB = __ballot(e != 0);
-        if (EB) {
-            err = (int32_t)cd_rl((uint32_t)e, (uint32_t)__builtin_ctzll(EB));
+        cd_stage<CD_IN_RING1>(inr, src, base, avail, loaded, lane);
+        uint32_t nbase;
+        const uint32_t x = cd_discover(inr, imask, tokpos, base, in_len, lane, nbase);
+        const CdRound r = cd_decode(inr, imask, base, x, O, in_len, cap);
+        if (r.err) {
+            err = r.err;
             break;
         }
-        const uint32_t total = cd_rl(incl, 63u);           /* round output bytes */
-
-        /* ---- 4. output bytes, 64 per step ------------------------------ */
-        /* tokens sit in lanes in output order, so the owner of output byte b
-         * of a group is (tokens started before the group) + (token starts in
-         * the group at or below b) - 1: the starts are marked in LDS with the
-         * group's tag (gb + 1, never reused, so the marks need no clearing)
-         * and read back as one ballot */
-        uint32_t tbase = 0;          /* tokens started before the group */
-#ifdef LZF_CD_ABLATE_OUTPUT           /* diagnostic builds only: time discovery alone */
-        for (uint32_t g = 0; g < 0u; g += CD_LANES) {
-#else
-        for (uint32_t g = 0; g < total; g += CD_LANES) {
-#endif
-            const uint32_t gb = O + g;                     /* group's first output offset */
-            if (tok && Ot >= gb && Ot < gb + CD_LANES) mark[Ot - gb] = gb + 1u;
-            cd_fence();
-            const uint64_t S = __ballot(mark[lane] == gb + 1u);
-            const uint32_t le = __builtin_amdgcn_mbcnt_hi((uint32_t)(S >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)S, 0u)) +
-                                (uint32_t)((S >> lane) & 1ull);
-            const uint32_t k = tbase + le - 1u;
-            tbase += (uint32_t)__builtin_popcountll(S);
-            const uint32_t o = gb + lane;
-            const bool live = g + lane < total;
-            const uint32_t tInf = (uint32_t)__shfl((int)tinfo, (int)k);
-            uint32_t val = 0;
-            int ptr = -1;
-            if (live) {
-                if (tInf >> 31) {
-                    val = inr[(o + tInf) & imask];
-                } else {
-                    const uint32_t so = o - tInf;
-                    if (so >= gb) ptr = (int)(so - gb);
-                    else val = outr[so & omask];
-                }
-            }
-            /* in-group back-references (runs): pointer doubling */
-            while (__ballot(ptr >= 0)) {
-                const int pi = ptr >= 0 ? ptr : (int)lane;
-                const uint32_t pv = (uint32_t)__shfl((int)val, pi);
-                const int pp = __shfl(ptr, pi);
-                if (ptr >= 0) { val = pv; ptr = pp; }
-            }
-            if (live) {
-                outr[o & omask] = (uint8_t)val;
-                dst[o] = (uint8_t)val;
-            }
-            cd_fence();
-        }
-        O += total;
-        /* next round: the token after the last one of this round */
-        base = base + cd_rl(x + tsz, ntok - 1u);
+        cd_output<CD_IN_RING1>(inr, outr, omask, mark, dst, O, r.total, x < CD_ROUND, O + r.rel, r.tinfo, lane);
+        O += r.total;
+        base = nbase;
     }
     if (lane == 0) {
         bt.out_len[v] = err ? 0u : O;
@@ -316,16 +409,156 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
     }
 }
 
+/* the pipe's hand-over of one round: token table + header, double-buffered.
+ * tok[l] = rel (bits 0-15: <= 64 * 264) | literal flag (16) | info (17-31:
+ * back-ref distance <= 8192, or the low bits of the literal's input offset
+ * minus its output offset, all the input ring's mask keeps) */
+struct CdSlot {
+    uint32_t tok[CD_LANES];
+    uint32_t ntok, total, last;
+    int32_t err;
+};
+/* the pipe's input ring: the consumer reads round k's literals,
+ * [base_k, base_k + 161), while the producer stages for round k + 1: staging
+ * runs when fewer than 192 bytes are ahead of base and fills up to base + 320
+ * (16-byte aligned), so it overwrites only bytes before
+ * base_{k+1} + 320 - 512 <= base_k - 32 (base_{k+1} <= base_k + 160) */
+#define CD_IN_RINGP 512u
+
+__device__ __forceinline__ void cd_stage_pipe(uint8_t *inr, const uint8_t *src, uint32_t base, uint32_t avail,
+                                              uint32_t &loaded, uint32_t lane)
+{
+    const uint32_t need = min(avail, base + 192u);
+    if (loaded < need) {
+        const uint32_t to = min(avail, (base + 320u) & ~15u);
+        const uint32_t x = loaded + 16u * lane;       /* loaded is a multiple of 16 here */
+        if (x < to) *(uint4 *)(inr + (x & (CD_IN_RINGP - 1u))) = cd_ld16(src + x, to - x);
+        loaded = to;
+        cd_fence();
+    }
+}
+
+__global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, uint32_t out_ring)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t *inr = smem;                               /* CD_IN_RINGP */
+    CdSlot *slot = (CdSlot *)(smem + CD_IN_RINGP);     /* 2 */
+    uint32_t *mark = (uint32_t *)(slot + 2);           /* the consumer's 64 token-start marks */
+    uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* the walk's token starts (CD_WALK) */
+    uint8_t *outr = tokpos + (CD_WALK ? CD_LANES : 0u);   /* out_ring (power of two) */
+    const uint32_t imask = CD_IN_RINGP - 1u, omask = out_ring - 1u;
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool producer = threadIdx.x < 64u;
+    const uint32_t v = blockIdx.x;
+    if ((bt.skip && bt.skip[v]) || cd_refused(bt, v, threadIdx.x)) return;
+    const uint32_t in_len = bt.in_len[v];
+    const uint32_t cap = bt.out_cap[v];
+
+    uint64_t tw[3] = {0ull, 0ull, 0ull};
+#ifdef CD_TIMING
+    tw[2] = __builtin_amdgcn_s_memtime();
+#endif
+    if (producer) {
+        /* steps 1-3, one round ahead of the consumer; round k's table goes to
+         * slot k & 1, published by the barrier that ends round k */
+        const uint8_t *src = bt.in + bt.in_off[v];
+        const uint32_t avail = in_len ? in_len : 1u;   /* a 0-length stream still reads one byte */
+        uint32_t loaded = 0, base = 0, O = 0;
+        for (uint32_t k = 0;; k++) {
+            cd_stage_pipe(inr, src, base, avail, loaded, lane);
+            uint32_t nbase;
+            const uint32_t x = cd_discover(inr, imask, tokpos, base, in_len, lane, nbase);
+            const CdRound r = cd_decode(inr, imask, base, x, O, in_len, cap);
+            const uint32_t ntok = (uint32_t)__builtin_popcountll(__ballot(x < CD_ROUND));
+            const uint32_t total = r.total;
+            CdSlot &s = slot[k & 1u];
+            s.tok[lane] = (r.rel & 0xFFFFu) | ((r.tinfo >> 31) << 16) | ((r.tinfo & 0x7FFFu) << 17);
+            const bool last = r.err != 0 || nbase >= in_len;   /* src/lzf_d.c:146 */
+            if (lane == 0) {
+                s.ntok = ntok;
+                s.total = total;
+                s.last = last;
+                s.err = r.err;
+            }
+            O += total;
+            base = nbase;
+            cd_barrier(tw);
+            if (last) break;
+        }
+    } else {
+        uint8_t *dst = bt.out + bt.out_off[v];
+        uint32_t O = 0;
+        int32_t err = 0;
+        mark[lane] = 0u;        /* group tags are >= 1 */
+        cd_barrier();
+        for (uint32_t k = 0;; k++) {
+            const CdSlot &s = slot[k & 1u];
+            const uint32_t total = __builtin_amdgcn_readfirstlane(s.total);
+            const uint32_t last = __builtin_amdgcn_readfirstlane(s.last);
+            const uint32_t ntok = __builtin_amdgcn_readfirstlane(s.ntok);
+            err = __builtin_amdgcn_readfirstlane(s.err);
+            if (err) break;      /* the failing round writes nothing */
+            const uint32_t w = s.tok[lane];
+            cd_output<CD_IN_RINGP>(inr, outr, omask, mark, dst, O, total, lane < ntok, O + (w & 0xFFFFu),
+                                   (w >> 17) | ((w & 0x10000u) << 15), lane);
+            O += total;
+            if (last) break;
+            cd_barrier(tw);
+        }
+#ifdef CD_TIMING
+        tw[0] += __builtin_amdgcn_s_memtime() - tw[2];
+#endif
+        if (lane == 0) {
+            bt.out_len[v] = err ? 0u : O;
+            bt.err[v] = err;
+        }
+    }
+#ifdef CD_TIMING
+    if (lane == 0) {
+        atomicAdd(&cd_tstat[producer ? 0 : 2], (unsigned long long)tw[0]);
+        atomicAdd(&cd_tstat[producer ? 1 : 3], (unsigned long long)tw[1]);
+    }
+#endif
+}
+
+/* the pipe for 8 KiB windows (values over 4 KiB); smaller windows leave
+ * room for twice the streams per CU as single waves, which the pipe's two
+ * waves per stream cannot use (32 waves per CU) */
+#ifndef CD_PIPE_MIN_RING
+#define CD_PIPE_MIN_RING 8192u
+#endif
+
 hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s)
 {
     uint32_t ring = 256u;
     while (ring < b.max_len && ring < CD_OUT_MAX) ring <<= 1;
-    const size_t lds = CD_IN_RING + ring + CD_LANES * 4u;     /* + the 64 marks */
-    hipError_t e = hipFuncSetAttribute((const void *)lzf_decompress_tokpar_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(lzf_decompress_tokpar_kernel, dim3(b.count), dim3(CD_LANES), lds, s, b, ring);
+    hipError_t e;
+    if (CD_PIPE && ring >= CD_PIPE_MIN_RING) {
+        const size_t lds = CD_IN_RINGP + 2u * sizeof(CdSlot) + 4u * CD_LANES + (CD_WALK ? CD_LANES : 0u) + ring;
+        e = hipFuncSetAttribute((const void *)lzf_decompress_pipe_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(lzf_decompress_pipe_kernel, dim3(b.count), dim3(2u * CD_LANES), lds, s, b, ring);
+    } else {
+        const size_t lds = CD_IN_RING1 + ring + CD_LANES * 5u;     /* + the 64 marks and token starts */
+        e = hipFuncSetAttribute((const void *)lzf_decompress_tokpar_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(lzf_decompress_tokpar_kernel, dim3(b.count), dim3(CD_LANES), lds, s, b, ring);
+    }
     return hipGetLastError();
 }
 
-const char *lzf_decompress_kernel_name(void) { return "tokpar64"; }
+#ifdef CD_TIMING
+/* producer busy, producer waiting, consumer busy, consumer waiting (cycles,
+ * summed over waves since the last call) */
+extern "C" int lzf_gpu_dec_tstat(unsigned long long *out)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cd_tstat), sizeof(cd_tstat)) != hipSuccess) return -1;
+    static const unsigned long long z[8] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(cd_tstat), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
+
+const char *lzf_decompress_kernel_name(void) { return CD_PIPE ? "pipe" : "tokpar64"; }
