@@ -305,11 +305,19 @@ __device__ __forceinline__ CdRound cd_decode(const uint8_t *inr, uint32_t imask,
  * in lanes in output order, so the owner of output byte b of a group is
  * (tokens started before the group) + (token starts in the group at or below
  * b) - 1: the starts are marked in LDS with the group's tag (gb + 1, never
- * reused, so the marks need no clearing) and read back as one ballot */
+ * reused, so the marks need no clearing) and read back as one ballot.  Byte
+ * sources are selected without branches (each branch costs the wave its
+ * exec-mask juggling); a byte's state is one word -- resolved (bit 16 |
+ * value) or the group lane holding its source (bits 8-13, a back-reference
+ * into the same group: src/lzf_d.c:137-142 copies byte-serially, so overlap
+ * replicates); a doubling step takes over the pointed-to lane's word (a
+ * resolved source resolves it, a pending one doubles the pointer).  Idle
+ * lanes store their byte to a sink slot; every group goes to HBM as it
+ * completes */
 template <uint32_t IN_RING>
-__device__ __forceinline__ void cd_output(const uint8_t *inr, uint8_t *outr, uint32_t omask, uint32_t *mark,
-                                          uint8_t *dst, uint32_t O, uint32_t total, bool tok, uint32_t Ot,
-                                          uint32_t tinfo, uint32_t lane)
+__device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint32_t omask, uint32_t *mark,
+                                             uint32_t sink_off, uint8_t *dst, uint32_t O, uint32_t total, bool tok,
+                                             uint32_t Ot, uint32_t tinfo, uint32_t lane)
 {
     constexpr uint32_t imask = IN_RING - 1u;
     uint32_t tbase = 0;          /* tokens started before the group */
@@ -318,7 +326,7 @@ __device__ __forceinline__ void cd_output(const uint8_t *inr, uint8_t *outr, uin
 #endif
     for (uint32_t g = 0; g < total; g += CD_LANES) {
         const uint32_t gb = O + g;                     /* group's first output offset */
-        if (tok && Ot >= gb && Ot < gb + CD_LANES) mark[Ot - gb] = gb + 1u;
+        if (tok && Ot - gb < CD_LANES) mark[Ot - gb] = gb + 1u;
         cd_fence();
         const uint64_t S = __ballot(mark[lane] == gb + 1u);
         const uint32_t le = __builtin_amdgcn_mbcnt_hi((uint32_t)(S >> 32),
@@ -326,31 +334,20 @@ __device__ __forceinline__ void cd_output(const uint8_t *inr, uint8_t *outr, uin
                             (uint32_t)((S >> lane) & 1ull);
         const uint32_t k = tbase + le - 1u;
         tbase += (uint32_t)__builtin_popcountll(S);
+        const uint32_t tInf = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)tinfo);
         const uint32_t o = gb + lane;
+        const uint32_t lit = (uint32_t)((int32_t)tInf >> 31);
+        const uint32_t so = o - tInf;
+        const uint32_t a = (((o + tInf) & imask) & lit) | ((outr_off + (so & omask)) & ~lit);
+        const uint32_t q = so - gb;
+        const uint32_t b = lds[a];
+        uint32_t ent = (!lit && q < CD_LANES) ? (q << 8) : (0x10000u | b);
+        while (__ballot(!(ent & 0x10000u)))
+            ent = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((ent & 0x10000u) ? lane : (ent >> 8)) << 2), (int)ent);
         const bool live = g + lane < total;
-        const uint32_t tInf = (uint32_t)__shfl((int)tinfo, (int)k);
-        uint32_t val = 0;
-        int ptr = -1;
-        if (live) {
-            if (tInf >> 31) {
-                val = inr[(o + tInf) & imask];
-            } else {
-                const uint32_t so = o - tInf;
-                if (so >= gb) ptr = (int)(so - gb);
-                else val = outr[so & omask];
-            }
-        }
-        /* in-group back-references (runs): pointer doubling */
-        while (__ballot(ptr >= 0)) {
-            const int pi = ptr >= 0 ? ptr : (int)lane;
-            const uint32_t pv = (uint32_t)__shfl((int)val, pi);
-            const int pp = __shfl(ptr, pi);
-            if (ptr >= 0) { val = pv; ptr = pp; }
-        }
-        if (live) {
-            outr[o & omask] = (uint8_t)val;
-            dst[o] = (uint8_t)val;
-        }
+        lds[live ? outr_off + (o & omask) : sink_off] = (uint8_t)ent;
+        if (g + CD_LANES <= total) dst[o] = (uint8_t)ent;
+        else if (live) dst[o] = (uint8_t)ent;
         cd_fence();
     }
 }
@@ -399,7 +396,8 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
             err = r.err;
             break;
         }
-        cd_output<CD_IN_RING1>(inr, outr, omask, mark, dst, O, r.total, x < CD_ROUND, O + r.rel, r.tinfo, lane);
+        cd_output<CD_IN_RING1>(smem, CD_IN_RING1, omask, mark, (uint32_t)(tokpos - smem), dst, O, r.total,
+                               x < CD_ROUND, O + r.rel, r.tinfo, lane);
         O += r.total;
         base = nbase;
     }
@@ -444,8 +442,8 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
     uint8_t *inr = smem;                               /* CD_IN_RINGP */
     CdSlot *slot = (CdSlot *)(smem + CD_IN_RINGP);     /* 2 */
     uint32_t *mark = (uint32_t *)(slot + 2);           /* the consumer's 64 token-start marks */
-    uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* the walk's token starts (CD_WALK) */
-    uint8_t *outr = tokpos + (CD_WALK ? CD_LANES : 0u);   /* out_ring (power of two) */
+    uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* the walk's token starts (CD_WALK); the sink */
+    uint8_t *outr = tokpos + CD_LANES;                 /* out_ring (power of two) */
     const uint32_t imask = CD_IN_RINGP - 1u, omask = out_ring - 1u;
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -500,8 +498,8 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
             err = __builtin_amdgcn_readfirstlane(s.err);
             if (err) break;      /* the failing round writes nothing */
             const uint32_t w = s.tok[lane];
-            cd_output<CD_IN_RINGP>(inr, outr, omask, mark, dst, O, total, lane < ntok, O + (w & 0xFFFFu),
-                                   (w >> 17) | ((w & 0x10000u) << 15), lane);
+            cd_output<CD_IN_RINGP>(smem, (uint32_t)(outr - smem), omask, mark, (uint32_t)(tokpos - smem), dst, O,
+                                   total, lane < ntok, O + (w & 0xFFFFu), (w >> 17) | ((w & 0x10000u) << 15), lane);
             O += total;
             if (last) break;
             cd_barrier(tw);
@@ -535,7 +533,7 @@ hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s)
     while (ring < b.max_len && ring < CD_OUT_MAX) ring <<= 1;
     hipError_t e;
     if (CD_PIPE && ring >= CD_PIPE_MIN_RING) {
-        const size_t lds = CD_IN_RINGP + 2u * sizeof(CdSlot) + 4u * CD_LANES + (CD_WALK ? CD_LANES : 0u) + ring;
+        const size_t lds = CD_IN_RINGP + 2u * sizeof(CdSlot) + 5u * CD_LANES + ring;
         e = hipFuncSetAttribute((const void *)lzf_decompress_pipe_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
