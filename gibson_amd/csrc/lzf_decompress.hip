@@ -209,33 +209,34 @@ __device__ __forceinline__ uint32_t cd_discover(const uint8_t *inr, uint32_t ima
 #else
     (void)tokpos;
     /* jump tables J0..J5 over the round's 128 positions packed two per lane
-     * (16 bits each; 128 = leaves the round).  A round holds <= 64 tokens
-     * (each takes >= 2 bytes): lane l finds the start of token l with six
-     * doubling levels */
+     * as bytes (bits 0-7: position 2l, 8-15: 2l + 1).  Leaving the round is
+     * 255, which reads lane 63's odd half -- position 127, whose token always
+     * leaves the round -- so 255 maps to itself at every level and no level
+     * tests for it.  A round holds <= 64 tokens (each takes >= 2 bytes):
+     * lane l finds the start of token l with six doubling levels */
     uint32_t PJ[6];
     {
-        const uint32_t ipa = base + pa, ipb = ipa + 1u;
+        const uint32_t ipa = base + pa;
         uint32_t na = pa + ta, nb = pb + tb;
-        if (ipa + ta >= in_len || na > CD_ROUND) na = CD_ROUND;
-        if (ipb + tb >= in_len || nb > CD_ROUND) nb = CD_ROUND;
-        PJ[0] = na | (nb << 16);
+        if (ipa + ta >= in_len || na >= CD_ROUND) na = 255u;
+        if (ipa + 1u + tb >= in_len || nb >= CD_ROUND) nb = 255u;
+        PJ[0] = na | (nb << 8);
     }
 #pragma unroll
     for (uint32_t k = 1; k < 6u; k++) {
-        const uint32_t ja = PJ[k - 1u] & 0xFFFFu, jb = PJ[k - 1u] >> 16;
-        const uint32_t wa = (uint32_t)__shfl((int)PJ[k - 1u], (int)((ja >> 1) & 63u));
-        const uint32_t wb = (uint32_t)__shfl((int)PJ[k - 1u], (int)((jb >> 1) & 63u));
-        const uint32_t va = ja >= CD_ROUND ? CD_ROUND : ((ja & 1u) ? wa >> 16 : wa & 0xFFFFu);
-        const uint32_t vb = jb >= CD_ROUND ? CD_ROUND : ((jb & 1u) ? wb >> 16 : wb & 0xFFFFu);
-        PJ[k] = va | (vb << 16);
+        const uint32_t P = PJ[k - 1u], ja = P & 0xFFu, jb = (P >> 8) & 0xFFu;
+        const uint32_t wa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((ja & 0x7Eu) << 1), (int)P);
+        const uint32_t wb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((jb & 0x7Eu) << 1), (int)P);
+        PJ[k] = ((wa >> ((ja & 1u) << 3)) & 0xFFu) | (((wb >> ((jb & 1u) << 3)) & 0xFFu) << 8);
     }
     uint32_t x = 0;
 #pragma unroll
     for (uint32_t b = 0; b < 6u; b++) {
-        const uint32_t w = (uint32_t)__shfl((int)PJ[b], (int)((x >> 1) & 63u));
-        const uint32_t y = (x & 1u) ? w >> 16 : w & 0xFFFFu;
-        if (((lane >> b) & 1u) && x < CD_ROUND) x = y;
+        const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((x & 0x7Eu) << 1), (int)PJ[b]);
+        const uint32_t y = (w >> ((x & 1u) << 3)) & 0xFFu;
+        x = ((lane >> b) & 1u) ? y : x;
     }
+    if (x >= CD_ROUND) x = CD_ROUND;
     /* the next round starts after the last token */
     const bool tok = x < CD_ROUND;
     const uint32_t ntok = (uint32_t)__builtin_popcountll(__ballot(tok));
@@ -262,16 +263,10 @@ __device__ __forceinline__ CdRound cd_decode(const uint8_t *inr, uint32_t imask,
     const uint32_t c = inr[ip & imask];
     const uint32_t b1 = inr[(ip + 1u) & imask], b2 = inr[(ip + 2u) & imask];
     const bool lit = c < 32u;
-    uint32_t olen, back = 0, lsrc = 0;
-    if (lit) {
-        olen = c + 1u;
-        lsrc = ip + 1u;
-    } else {
-        uint32_t len = c >> 5, offb = b1;
-        if (len == 7u) { len += b1; offb = b2; }
-        olen = len + 2u;
-        back = ((c & 31u) << 8) + offb + 1u;
-    }
+    const bool l7 = (c >> 5) == 7u;                     /* length in the next byte */
+    const uint32_t back = ((c & 31u) << 8) + (l7 ? b2 : b1) + 1u;   /* back-refs only */
+    const uint32_t olen = lit ? c + 1u : (c >> 5) + (l7 ? b1 : 0u) + 2u;
+    const uint32_t lsrc = ip + 1u;                      /* literals only */
     const uint32_t ol = tok ? olen : 0u;
     const uint32_t incl = cd_incl_sum(ol);
     CdRound r;
@@ -284,7 +279,7 @@ __device__ __forceinline__ CdRound cd_decode(const uint8_t *inr, uint32_t imask,
      * inside the cap, only a back-reference before the output start can fail */
     int32_t e = 0;
     if (base + CD_ROUND + 33u <= in_len && (uint64_t)O + r.total <= cap) {
-        if (tok && !lit && back > Ot) e = 22;                               /* :127 */
+        e = (tok && !lit && back > Ot) ? 22 : 0;                            /* :127 */
     } else if (tok) {
         if (lit) {
             if ((uint64_t)Ot + olen > cap) e = 7;                           /* E2BIG  :72 */
@@ -442,8 +437,9 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
     uint8_t *inr = smem;                               /* CD_IN_RINGP */
     CdSlot *slot = (CdSlot *)(smem + CD_IN_RINGP);     /* 2 */
     uint32_t *mark = (uint32_t *)(slot + 2);           /* the consumer's 64 token-start marks */
-    uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* the walk's token starts (CD_WALK); the sink */
-    uint8_t *outr = tokpos + CD_LANES;                 /* out_ring (power of two) */
+    uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* the walk's token starts (CD_WALK, producer) */
+    uint8_t *sink = tokpos + CD_LANES;                 /* the consumer's idle-lane byte sink */
+    uint8_t *outr = sink + 16u;                        /* out_ring (power of two) */
     const uint32_t imask = CD_IN_RINGP - 1u, omask = out_ring - 1u;
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -498,7 +494,7 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
             err = __builtin_amdgcn_readfirstlane(s.err);
             if (err) break;      /* the failing round writes nothing */
             const uint32_t w = s.tok[lane];
-            cd_output<CD_IN_RINGP>(smem, (uint32_t)(outr - smem), omask, mark, (uint32_t)(tokpos - smem), dst, O,
+            cd_output<CD_IN_RINGP>(smem, (uint32_t)(outr - smem), omask, mark, (uint32_t)(sink - smem), dst, O,
                                    total, lane < ntok, O + (w & 0xFFFFu), (w >> 17) | ((w & 0x10000u) << 15), lane);
             O += total;
             if (last) break;
@@ -533,7 +529,7 @@ hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s)
     while (ring < b.max_len && ring < CD_OUT_MAX) ring <<= 1;
     hipError_t e;
     if (CD_PIPE && ring >= CD_PIPE_MIN_RING) {
-        const size_t lds = CD_IN_RINGP + 2u * sizeof(CdSlot) + 5u * CD_LANES + ring;
+        const size_t lds = CD_IN_RINGP + 2u * sizeof(CdSlot) + 5u * CD_LANES + 16u + ring;
         e = hipFuncSetAttribute((const void *)lzf_decompress_pipe_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
