@@ -57,6 +57,14 @@
 #ifndef KT_BALLOT
 #define KT_BALLOT (KT_WIN > 7u)
 #endif
+/* table step as one lane-ordered 16-bit exchange per window (1; needs 15
+ * windows): ds_mskor_rtn_b32 on the dword holding the slot's half returns
+ * the latest same-slot position -- the table's or an earlier lane's of the
+ * same window -- and leaves the highest lane's, so A computes no same-slot
+ * lane masks (tools/lds_mskor_order.hip checks the lane order) */
+#ifndef KT_MSKOR
+#define KT_MSKOR 1
+#endif
 #define KT_BLK (64u * KT_WIN)
 #define KT_THREADS (64u * (KT_WIN + 1u))
 #ifndef KT_PF
@@ -74,6 +82,32 @@ __device__ __forceinline__ void kt_wave_fence()
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
 }
+
+#if KT_MSKOR
+static_assert(KT_WIN % 5u == 0u, "the exchanges go in groups of 5 windows");
+/* LDS byte address of a __shared__ object */
+__device__ __forceinline__ uint32_t kt_lds_addr(const void *p)
+{
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+/* five windows' exchanges, issued in window (= position) order, then one
+ * wait: the LDS writes the results after issue, so they are outputs of the
+ * same asm statement (early-clobber: no result shares an input's register)
+ * and nothing reads them before the wait.  Groups of five keep the table
+ * wave's live registers inside the workers' budget (15 at once spills) */
+#define KT_X(i_) "ds_mskor_rtn_b32 %" #i_ ", %[a" #i_ "], %[m" #i_ "], %[d" #i_ "]\n\t"
+#define KT_IN(i_) [a##i_] "v"(a[i_]), [m##i_] "v"(m[i_]), [d##i_] "v"(d[i_])
+__device__ __forceinline__ void kt_xchg5(uint32_t (&r)[5], const uint32_t (&a)[5], const uint32_t (&m)[5],
+                                         const uint32_t (&d)[5])
+{
+    asm volatile(KT_X(0) KT_X(1) KT_X(2) KT_X(3) KT_X(4) "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4])
+                 : KT_IN(0), KT_IN(1), KT_IN(2), KT_IN(3), KT_IN(4)
+                 : "memory");
+}
+#undef KT_X
+#undef KT_IN
+#endif
 
 /* S entry of a position of the block */
 #define KS_ACT  (1u << 16)
@@ -153,6 +187,8 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
     const uint32_t j = w - 1u;                                 /* worker's window (w >= 1) */
     const unsigned long long mine = 1ull << lane, below = mine - 1ull;
+    (void)mine;
+    (void)below;
     const uint32_t np = n - 2u;                                /* positions 0 .. n-3, src/lzf_c.c:145 */
     const uint32_t nb = (np + KT_BLK - 1u) / KT_BLK;
     /* worker: the 8 bytes of its position in the next KT_PF blocks are in
@@ -210,6 +246,30 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 const uint32_t k = t - 1u, B = KT_BLK * k;
                 const uint32_t *Sk = S + KT_BLK * (k & 1u);
                 uint16_t *Ok = O + KT_BLK * (k % 3u);
+#if KT_MSKOR
+                /* a position past the value exchanges in its lane's own
+                 * dummy half (T[65536 + lane]) */
+                const uint32_t tb = kt_lds_addr(T);
+#pragma unroll
+                for (uint32_t g = 0; g < KT_WIN; g += 5u) {
+                    uint32_t xa[5], xm[5], xd[5], xr[5], xs[5];
+#pragma unroll
+                    for (uint32_t u = 0; u < 5u; u++) {
+                        const uint32_t i = g + u, e = Sk[64u * i + lane];
+                        const uint32_t h = (e & KS_ACT) ? (e & 0xFFFFu) : LZF_SLOTS + lane;
+                        xs[u] = (h & 1u) << 4;
+                        xa[u] = tb + 4u * (h >> 1);
+                        xm[u] = 0xFFFFu << xs[u];
+                        xd[u] = ((B + 64u * i + lane) & 0xFFFFu) << xs[u];
+                    }
+                    kt_xchg5(xr, xa, xm, xd);
+#pragma unroll
+                    for (uint32_t u = 0; u < 5u; u++) Ok[64u * (g + u) + lane] = (uint16_t)(xr[u] >> xs[u]);
+                }
+                if (false) {
+#else
+                if (true) {
+#endif
                 uint32_t e[KT_WIN], tv[KT_WIN];
 #pragma unroll
                 for (uint32_t i = 0; i < KT_WIN; i++) e[i] = Sk[64u * i + lane];
@@ -227,6 +287,7 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
 #pragma unroll
                 for (uint32_t i = 0; i < KT_WIN; i++)
                     Ok[64u * i + lane] = (uint16_t)((e[i] & KS_PRED) ? B + 64u * i + ((e[i] >> KS_PL) & 63u) : tv[i]);
+                }
             }
         } else {
             /* ---- C2(t-3): agreement and record; Q <- O of that block ------- */
@@ -284,6 +345,9 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 const uint2 a = pf[PS];
                 ak[PS] = a;
                 const uint32_t s = dv_slot(a.x);
+#if KT_MSKOR
+                S[KT_BLK * (t & 1u) + 64u * j + lane] = act ? (s | KS_ACT) : 0u;
+#else
 #if KT_BALLOT
                 /* exact: the lanes agreeing with mine on every slot bit.  Per
                  * bit: x = my bit sign-extended (0 / ~0), its ballot bb, and
@@ -321,6 +385,7 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 S[KT_BLK * (t & 1u) + 64u * j + lane] =
                     act ? (s | KS_ACT | (pb ? KS_PRED : 0u) | ((M >> lane) == 1ull ? KS_LAST : 0u) | (pl << KS_PL))
                         : 0u;
+#endif
             }
         }
         if (w) KT_TM(4);
