@@ -70,6 +70,12 @@
 #ifndef KT_PF
 #define KT_PF 4u                /* blocks of input bytes in flight per lane */
 #endif
+#ifndef KT_BF
+#define KT_BF 1                 /* C1/C2 without divergent branches (selects) */
+#endif
+#ifndef KT_CL
+#define KT_CL 2u                /* steps from C1 (agreement loads issued) to C2 (consumed); divides KT_PF */
+#endif
 
 __device__ __forceinline__ uint32_t kt_code(uint32_t k)
 {
@@ -105,8 +111,28 @@ __device__ __forceinline__ void kt_xchg5(uint32_t (&r)[5], const uint32_t (&a)[5
                  : KT_IN(0), KT_IN(1), KT_IN(2), KT_IN(3), KT_IN(4)
                  : "memory");
 }
+__device__ __forceinline__ void kt_xchg15(uint32_t (&r)[15], const uint32_t (&a)[15], const uint32_t (&m)[15],
+                                          const uint32_t (&d)[15])
+{
+    asm volatile(KT_X(0) KT_X(1) KT_X(2) KT_X(3) KT_X(4) KT_X(5) KT_X(6) KT_X(7) KT_X(8) KT_X(9) KT_X(10) KT_X(11)
+                     KT_X(12) KT_X(13) KT_X(14) "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]),
+                   "=&v"(r[7]), "=&v"(r[8]), "=&v"(r[9]), "=&v"(r[10]), "=&v"(r[11]), "=&v"(r[12]), "=&v"(r[13]),
+                   "=&v"(r[14])
+                 : KT_IN(0), KT_IN(1), KT_IN(2), KT_IN(3), KT_IN(4), KT_IN(5), KT_IN(6), KT_IN(7), KT_IN(8),
+                   KT_IN(9), KT_IN(10), KT_IN(11), KT_IN(12), KT_IN(13), KT_IN(14)
+                 : "memory");
+}
 #undef KT_X
 #undef KT_IN
+#endif
+/* exchanges per asm group (5 or 15) and whether the group's S entries are
+ * all read before the first group (1) */
+#ifndef KT_XG
+#define KT_XG 5
+#endif
+#ifndef KT_SHOIST
+#define KT_SHOIST 0
 #endif
 
 /* S entry of a position of the block */
@@ -214,14 +240,23 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
      * never a ref, and a candidate 0 decides like no candidate) */
     for (uint32_t k = tid; k < LZF_SLOTS / 8u; k += KT_THREADS) ((uint4 *)T)[k] = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    /* C1 -> C2 state of the worker's window */
-    uint32_t c_p = 0xFFFFFFFFu, c_q1 = 0u, c_q2 = 0u, c_avail = 0u;
-    uint2 c_a = make_uint2(0u, 0u), c_b1 = c_a, c_b2 = c_a;
+    /* C1 -> C2 state of the worker's window: KT_CL sets, so the agreement
+     * loads C1 issues are consumed KT_CL steps later (one step of slack puts
+     * a load latency on every step's critical path) */
+    uint32_t c_p[KT_CL], c_q1[KT_CL], c_q2[KT_CL], c_avail[KT_CL];
+    uint2 c_a[KT_CL], c_b1[KT_CL], c_b2[KT_CL];
+#pragma unroll
+    for (uint32_t i = 0; i < KT_CL; i++) {
+        c_p[i] = 0xFFFFFFFFu;
+        c_q1[i] = c_q2[i] = c_avail[i] = 0u;
+        c_a[i] = c_b1[i] = c_b2[i] = make_uint2(0u, 0u);
+    }
 #ifdef KT_TIMING
     uint64_t kt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
     const auto step = [&](auto ps, auto clamp, uint32_t t) {
         constexpr uint32_t PS = decltype(ps)::value;             /* t % KT_PF */
+        constexpr uint32_t CS = PS % KT_CL;                      /* C1 -> C2 set of this step */
         /* CLAMP: the step's loads may reach past the value (its last
          * blocks); otherwise they are plain 8-byte loads */
         constexpr bool CLAMP = SMALL || decltype(clamp)::value != 0u;
@@ -250,21 +285,35 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 /* a position past the value exchanges in its lane's own
                  * dummy half (T[65536 + lane]) */
                 const uint32_t tb = kt_lds_addr(T);
+#if KT_SHOIST
+                uint32_t se[KT_WIN];
 #pragma unroll
-                for (uint32_t g = 0; g < KT_WIN; g += 5u) {
-                    uint32_t xa[5], xm[5], xd[5], xr[5], xs[5];
+                for (uint32_t i = 0; i < KT_WIN; i++) se[i] = Sk[64u * i + lane];
+#endif
 #pragma unroll
-                    for (uint32_t u = 0; u < 5u; u++) {
-                        const uint32_t i = g + u, e = Sk[64u * i + lane];
+                for (uint32_t g = 0; g < KT_WIN; g += KT_XG) {
+                    uint32_t xa[KT_XG], xm[KT_XG], xd[KT_XG], xr[KT_XG], xs[KT_XG];
+#pragma unroll
+                    for (uint32_t u = 0; u < KT_XG; u++) {
+                        const uint32_t i = g + u;
+#if KT_SHOIST
+                        const uint32_t e = se[i];
+#else
+                        const uint32_t e = Sk[64u * i + lane];
+#endif
                         const uint32_t h = (e & KS_ACT) ? (e & 0xFFFFu) : LZF_SLOTS + lane;
                         xs[u] = (h & 1u) << 4;
                         xa[u] = tb + 4u * (h >> 1);
                         xm[u] = 0xFFFFu << xs[u];
                         xd[u] = ((B + 64u * i + lane) & 0xFFFFu) << xs[u];
                     }
+#if KT_XG == 15
+                    kt_xchg15(xr, xa, xm, xd);
+#else
                     kt_xchg5(xr, xa, xm, xd);
+#endif
 #pragma unroll
-                    for (uint32_t u = 0; u < 5u; u++) Ok[64u * (g + u) + lane] = (uint16_t)(xr[u] >> xs[u]);
+                    for (uint32_t u = 0; u < KT_XG; u++) Ok[64u * (g + u) + lane] = (uint16_t)(xr[u] >> xs[u]);
                 }
                 if (false) {
 #else
@@ -290,41 +339,74 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 }
             }
         } else {
-            /* ---- C2(t-3): agreement and record; Q <- O of that block ------- */
+            /* ---- C2(t-2-KT_CL): agreement and record ------------------------ */
+            if (c_p[CS] < np) {
+                const uint32_t cp = c_p[CS], cq1 = c_q1[CS], cq2 = c_q2[CS], cav = c_avail[CS];
+                const uint2 ca = c_a[CS], cb1 = c_b1[CS], cb2 = c_b2[CS];
+#if KT_BF
+                /* branch-free: both agreements always, the record by selects */
+                const uint64_t x1 = ((uint64_t)(ca.y ^ cb1.y) << 32) | (uint64_t)(ca.x ^ cb1.x);
+                const uint64_t x2 = ((uint64_t)(ca.y ^ cb2.y) << 32) | (uint64_t)(ca.x ^ cb2.x);
+                const uint32_t k1 = min(x1 ? (uint32_t)__builtin_ctzll(x1) >> 3 : 8u, cav);
+                const uint32_t k2 = min(x2 ? (uint32_t)__builtin_ctzll(x2) >> 3 : 8u, cav);
+                const uint32_t r1 = (cp - cq1 - 1u) | (kt_code(k1) << 13);
+                const uint32_t r2 = ((cp - cq2 - 1u) | (kt_code(k2) << 13)) << 16;
+                rec[cp] = cq1 ? (r1 | (cq2 ? r2 : 0u)) : 0u;
+#else
+                uint32_t r = 0u;
+                if (cq1) {
+                    const uint64_t x1 = ((uint64_t)(ca.y ^ cb1.y) << 32) | (uint64_t)(ca.x ^ cb1.x);
+                    uint32_t k1 = x1 ? (uint32_t)__builtin_ctzll(x1) >> 3 : 8u;
+                    k1 = k1 < cav ? k1 : cav;
+                    r = (cp - cq1 - 1u) | (kt_code(k1) << 13);
+                    if (cq2) {
+                        const uint64_t x2 = ((uint64_t)(ca.y ^ cb2.y) << 32) | (uint64_t)(ca.x ^ cb2.x);
+                        uint32_t k2 = x2 ? (uint32_t)__builtin_ctzll(x2) >> 3 : 8u;
+                        k2 = k2 < cav ? k2 : cav;
+                        r |= ((cp - cq2 - 1u) | (kt_code(k2) << 13)) << 16;
+                    }
+                }
+                rec[cp] = r;
+#endif
+            }
+            /* ---- Q <- O of block t-3 ---------------------------------------- */
             if (t >= 3u && t - 3u < nb) {
                 const uint32_t k = t - 3u;
-                if (c_p < np) {
-                    uint32_t r = 0u;
-                    if (c_q1) {
-                        const uint64_t x1 = ((uint64_t)(c_a.y ^ c_b1.y) << 32) | (uint64_t)(c_a.x ^ c_b1.x);
-                        uint32_t k1 = x1 ? (uint32_t)__builtin_ctzll(x1) >> 3 : 8u;
-                        k1 = k1 < c_avail ? k1 : c_avail;
-                        r = (c_p - c_q1 - 1u) | (kt_code(k1) << 13);
-                        if (c_q2) {
-                            const uint64_t x2 = ((uint64_t)(c_a.y ^ c_b2.y) << 32) | (uint64_t)(c_a.x ^ c_b2.x);
-                            uint32_t k2 = x2 ? (uint32_t)__builtin_ctzll(x2) >> 3 : 8u;
-                            k2 = k2 < c_avail ? k2 : c_avail;
-                            r |= ((c_p - c_q2 - 1u) | (kt_code(k2) << 13)) << 16;
-                        }
-                    }
-                    rec[c_p] = r;
-                }
                 const uint32_t x = KT_BLK * k + 64u * j + lane;
                 if (x < np) Q[x & (LZF_WINDOW - 1u)] = O[KT_BLK * (k % 3u) + 64u * j + lane];
             }
             KT_TM(2);
             /* ---- C1(t-2): q1, q2; their agreement loads below ---------------- */
-            c_p = 0xFFFFFFFFu;
-            c_q1 = c_q2 = 0u;
+            c_p[CS] = 0xFFFFFFFFu;
+            c_q1[CS] = c_q2[CS] = 0u;
             if (t >= 2u && t - 2u < nb) {
                 const uint32_t k = t - 2u, B = KT_BLK * k;
                 const uint32_t p = B + 64u * j + lane;
+#if KT_BF
+                /* branch-free: the Q..O read at a clamped index for every lane,
+                 * validity by selects */
+                const bool act = p < np;
+                const uint16_t *Ok = O + KT_BLK * (k % 3u);
+                const uint32_t q1r = Ok[64u * j + lane];
+                const uint32_t q1 = act && p - q1r <= LZF_WINDOW ? q1r : 0u;   /* q1r = 0: none */
+                const uint32_t ik = LZF_WINDOW + KT_BLK * (k % 3u), ip = LZF_WINDOW + KT_BLK * ((k + 2u) % 3u);
+                const uint32_t iq = q1 >= B ? ik + (q1 - B)
+                                  : q1 + KT_BLK >= B ? ip + (q1 + KT_BLK - B)
+                                                     : (q1 & (LZF_WINDOW - 1u));
+                const uint32_t q2r = Q[iq];
+                const uint32_t q2 = q1 && q2r != 0u && p - q2r <= LZF_WINDOW ? q2r : 0u;
+                c_p[CS] = act ? p : 0xFFFFFFFFu;
+                c_avail[CS] = n - p;
+                c_a[CS] = ak[(PS + KT_PF - 2u) % KT_PF];              /* A's bytes of block t-2 */
+                c_q1[CS] = l1 = q1;
+                c_q2[CS] = l2 = q2;
+#else
                 if (p < np) {
-                    c_p = p;
+                    c_p[CS] = p;
                     const uint16_t *Ok = O + KT_BLK * (k % 3u);
                     const uint32_t q1 = Ok[64u * j + lane];
-                    c_avail = n - p;
-                    c_a = ak[(PS + KT_PF - 2u) % KT_PF];              /* A's bytes of block t-2 */
+                    c_avail[CS] = n - p;
+                    c_a[CS] = ak[(PS + KT_PF - 2u) % KT_PF];          /* A's bytes of block t-2 */
                     if (q1 != 0u && p - q1 <= LZF_WINDOW) {          /* off = p - q - 1 < 8192 */
                         /* Ok / Op / the ring, as one index into Q..O */
                         const uint32_t ik = LZF_WINDOW + KT_BLK * (k % 3u), ip = LZF_WINDOW + KT_BLK * ((k + 2u) % 3u);
@@ -332,10 +414,11 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                                           : q1 + KT_BLK >= B ? ip + (q1 + KT_BLK - B)
                                                              : (q1 & (LZF_WINDOW - 1u));
                         const uint32_t q2 = Q[iq];
-                        c_q1 = l1 = q1;
-                        if (q2 != 0u && p - q2 <= LZF_WINDOW) c_q2 = l2 = q2;
+                        c_q1[CS] = l1 = q1;
+                        if (q2 != 0u && p - q2 <= LZF_WINDOW) c_q2[CS] = l2 = q2;
                     }
                 }
+#endif
             }
             KT_TM(3);
             /* ---- A(t): the worker's window of block t ----------------------- */
@@ -395,8 +478,8 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
 #ifdef KT_ABL_C
         l1 = l2 = 0u;
 #endif
-        c_b1 = ld8(l1);
-        c_b2 = ld8(l2);
+        c_b1[CS] = ld8(l1);
+        c_b2[CS] = ld8(l2);
         pf[PS] = ld8(lp);
         if (w) KT_TM(5);
 #ifndef KT_ABL_S
@@ -413,13 +496,15 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
      * the end-of-value clamp (the last group of steps keeps it) */
     uint32_t t = 0;
     if (!SMALL)
-        for (; t < nb + 3u && KT_BLK * (t + 3u + KT_PF + 1u) + 8u <= n; t += KT_PF) {
+        for (; t < nb + 2u + KT_CL && KT_BLK * (t + 3u + KT_PF + 1u) + 8u <= n; t += KT_PF) {
             step(KtIc<0>{}, KtIc<0>{}, t);
             step(KtIc<1>{}, KtIc<0>{}, t + 1u);
             step(KtIc<2>{}, KtIc<0>{}, t + 2u);
             step(KtIc<3>{}, KtIc<0>{}, t + 3u);
         }
-    for (; t < nb + 3u; t += KT_PF) {
+    /* (a per-step tail, to run no empty steps past the last, measured
+     * slower: its switch costs more than the steps it saves) */
+    for (; t < nb + 2u + KT_CL; t += KT_PF) {
         step(KtIc<0>{}, KtIc<1>{}, t);
         step(KtIc<1>{}, KtIc<1>{}, t + 1u);
         step(KtIc<2>{}, KtIc<1>{}, t + 2u);

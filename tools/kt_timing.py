@@ -36,9 +36,10 @@ e1.record()
 torch.cuda.synchronize()
 L.lzf_gpu_debug_kt(buf, 0)
 v = list(buf)
-steps = v[7] / 8  # steps counted by every wave (8 per workgroup)
+nw = int(os.environ.get("KT_WIN", "15"))  # worker waves per workgroup
+steps = v[7] / (nw + 1)  # steps counted by every wave
 names = ["B (table wave)", "table wave barrier", "C2", "C1", "A", "worker loads", "worker barrier"]
 print(f"kernel {e0.elapsed_time(e1):.2f} ms, {steps:.0f} workgroup-steps")
 for i, nm in enumerate(names):
-    per = v[i] / steps / (1 if i < 2 else 7)
+    per = v[i] / steps / (1 if i < 2 else nw)
     print(f"  {nm:22s} {per:9.1f} cycles per step (per wave)")
