@@ -836,7 +836,15 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
                     word = (q > ms && q + 3u <= me) ? 0u : 0xFFFFFFFFu;         /* last match's interior */
                 } else {
                     const uint32_t d = cw - (q >> 5);
+#ifdef K3_DUPBITS   /* diagnostic: a second line per scratch bitmap word, same wait */
+                    if (d != 0u && (q >> 5) < fl) {
+                        const uint32_t x_ = bits[(q >> 5) ^ 64u];
+                        word = bits[q >> 5] | (x_ & bt.max_len & 0x80000000u);
+                    } else
+                        word = d == 0u ? curw : K3_RING(q >> 5);
+#else
                     word = d == 0u ? curw : (q >> 5) >= fl ? K3_RING(q >> 5) : bits[q >> 5];
+#endif
 #ifdef KT_TIMING
                     if (d && (q >> 5) < fl) K3_CNT(12);
 #endif
@@ -855,7 +863,11 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
                     qn = 0xFFFFFFFFu;
                 } else if (qn == 0xFFFFFFFFu) {                              /* load q's record: two more links */
                     K3_CNT(13);
+#ifdef K3_DUPREC    /* diagnostic: a second line per record hop, same wait */
+                    const uint32_t c2 = rec[q] | (rec[q ^ 64u] & bt.max_len & 0x80000000u);
+#else
                     const uint32_t c2 = rec[q];
+#endif
                     const uint32_t r1 = (c2 >> 13) & 7u, r2 = c2 >> 29;
                     const uint32_t y1 = q - 1u - (c2 & 0x1FFFu), y2 = q - 1u - ((c2 >> 16) & 0x1FFFu);
                     if (!r1 || p - y1 - 1u >= LZF_WINDOW) {                  /* the chain leaves p's window */
