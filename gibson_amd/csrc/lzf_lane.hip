@@ -289,6 +289,11 @@ hipError_t lzf_launch_decompress_lane(const LzfBatch &b, hipStream_t s)
 #ifndef KS8_WIN
 #define KS8_WIN     2u            /* 8 KiB small class: windows per step */
 #endif
+/* small class: bucket heads by a lane-ordered exchange (1) instead of the
+ * digit lane bitmaps (0) */
+#ifndef KS_XCHG
+#define KS_XCHG     1
+#endif
 #define KS_MAXN     4096u         /* small class: 12-bit bucket, 4-bit identity, positions + 1 fit 12 bits */
 #define KS8_MAXN    8192u         /* small class, 8 KiB: 13-bit bucket, 3-bit identity, positions + 1 fit 13 bits */
 #define KM_BUCKETS  2048u         /* mid class */
@@ -403,15 +408,24 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
     constexpr uint32_t T2 = T1 + (1u << (10u - IDB));    /* digit m[0, IDB)      : 2^IDB entries */
     constexpr uint32_t TN = T2 + (1u << IDB);
     constexpr uint32_t PF = MAXN / 1024u;                /* 16-byte loads per lane per value */
-    __shared__ __attribute__((aligned(16))) uint16_t H[BUCKETS];
+    __shared__ __attribute__((aligned(16))) uint16_t H[BUCKETS + 64u];   /* + one dummy per lane (KS_XCHG) */
     __shared__ uint16_t E[MAXN];
     __shared__ __attribute__((aligned(16))) uint32_t Bw[MAXN / 4u + 4u];
+#if !KS_XCHG
     __shared__ unsigned long long T[WIN][TN];
+#endif
     const uint32_t lane = threadIdx.x;
     const unsigned long long mine = 1ull << lane, below = mine - 1ull;
     uint32_t v = blockIdx.x;
     if (v >= bt.count) return;
+#if KS_XCHG
+    (void)mine;
+    (void)below;
+    (void)T0;
+    (void)TN;
+#else
     for (uint32_t k = lane; k < WIN * TN; k += 64u) (&T[0][0])[k] = 0ull;
+#endif
     uint4 pf[PF];
     uint32_t pn = bt.in_len[v];
     {
@@ -451,6 +465,53 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                     act[j] = p[j] < np;
                     tri[j] = ks_rd4(Bw, act[j] ? p[j] : 0u);
                 }
+#if KS_XCHG
+                /* one lane-ordered 16-bit exchange per window on the bucket's
+                 * head (ds_mskor_rtn_b32, tools/lds_mskor_order.hip): each lane
+                 * gets the latest earlier position of its bucket -- the
+                 * head's or an earlier lane's of the window -- and the
+                 * highest lane's key stays.  The skip link of p is that
+                 * predecessor when its identity differs, else the
+                 * predecessor's own link (an earlier lane's: resolved by
+                 * pointer doubling over the window's lanes); the same-slot
+                 * predecessor follows the links from it until the identity
+                 * matches.  Windows go in order: window j's links are in E
+                 * before window j+1 exchanges. */
+                uint32_t q1[WIN], cur[WIN];
+                bool need = false;
+                const uint32_t hb = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)H;
+#pragma unroll
+                for (uint32_t j = 0; j < WIN; j++) {
+                    m[j] = ln_mix(ln_slot(tri[j]));
+                    const uint32_t id = m[j] & IDM;
+                    const uint32_t key = ((p[j] + 1u) << IDB) | id;
+                    const uint32_t h = act[j] ? (m[j] >> IDB) : BUCKETS + lane;
+                    const uint32_t sh = (h & 1u) << 4;
+                    uint32_t rv;
+                    asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
+                                 : "=&v"(rv)
+                                 : "v"(hb + 4u * (h >> 1)), "v"(0xFFFFu << sh), "v"(key << sh)
+                                 : "memory");
+                    const uint32_t prev = act[j] ? (rv >> sh) & 0xFFFFu : 0u;
+                    const uint32_t ppos = (prev >> IDB) - 1u;            /* prev != 0 */
+                    const uint32_t w0 = P + 64u * j;                      /* the window's first position */
+                    const bool same = prev && (prev & IDM) == id;
+                    /* link entry: resolved (bit 16 | link) or pending (the lane of
+                     * an earlier same-slot position of this window) */
+                    const uint32_t lprev = same && ppos < w0 ? (uint32_t)E[ppos] : 0u;
+                    uint32_t le = !same ? (0x10000u | prev) : ppos >= w0 ? (ppos - w0) : (0x10000u | lprev);
+                    while (__ballot(!(le & 0x10000u)))
+                        le = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((le & 0x10000u) ? lane : le) << 2), (int)le);
+                    if (act[j]) E[p[j]] = (uint16_t)le;
+                    ln_wave_fence();
+                    /* same-slot predecessor: prev if its identity is mine, else
+                     * along the links from prev's own link */
+                    q1[j] = same ? (prev >> IDB) : 0u;                    /* pos+1 */
+                    cur[j] = (prev && !same) ? (uint32_t)E[ppos] : 0u;
+                    if (cur[j] && (cur[j] & IDM) == id) { q1[j] = cur[j] >> IDB; cur[j] = 0u; }
+                    need |= cur[j] != 0u;
+                }
+#else
 #pragma unroll
                 for (uint32_t j = 0; j < WIN; j++) {
                     m[j] = ln_mix(ln_slot(tri[j]));
@@ -513,6 +574,7 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                     }
                     need |= cur[j] != 0u;
                 }
+#endif /* KS_XCHG */
                 ln_wave_fence();
 #ifdef KS_ABL_WALK
                 need = false;
