@@ -284,7 +284,7 @@ hipError_t lzf_launch_decompress_lane(const LzfBatch &b, hipStream_t s)
 
 #define K1_WIN      4u            /* windows of 64 positions resolved per step */
 #ifndef KS_WIN
-#define KS_WIN      2u            /* small class: windows per step (2: 31.4 ms, 1: 33.1, 3: 36.9, 4: 36.3 on json4k) */
+#define KS_WIN      4u            /* small class: windows per step (exchange form, json4k compress: 4: 48.6 ms, 3: 49.1, 2: 49.8, 1: 52.2) */
 #endif
 #ifndef KS8_WIN
 #define KS8_WIN     2u            /* 8 KiB small class: windows per step */
@@ -398,6 +398,37 @@ __device__ __forceinline__ uint32_t ks_hibit(uint64_t m)
     return 63u - (uint32_t)__builtin_clzll(m);
 }
 
+#if KS_XCHG
+/* WIN lane-ordered 16-bit exchanges (ds_mskor_rtn_b32), issued in order, one wait */
+template <uint32_t WIN>
+__device__ __forceinline__ void ks_xchg(uint32_t (&r)[WIN], const uint32_t (&a)[WIN], const uint32_t (&m)[WIN],
+                                        const uint32_t (&d)[WIN])
+{
+    static_assert(WIN >= 1u && WIN <= 4u, "1..4 windows per step");
+    if constexpr (WIN == 1u) {
+        asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(r[0]) : "v"(a[0]), "v"(m[0]), "v"(d[0]) : "memory");
+    } else if constexpr (WIN == 2u) {
+        asm volatile("ds_mskor_rtn_b32 %0, %2, %3, %4\n\tds_mskor_rtn_b32 %1, %5, %6, %7\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(r[0]), "=&v"(r[1])
+                     : "v"(a[0]), "v"(m[0]), "v"(d[0]), "v"(a[1]), "v"(m[1]), "v"(d[1]) : "memory");
+    } else if constexpr (WIN == 3u) {
+        asm volatile("ds_mskor_rtn_b32 %0, %3, %4, %5\n\tds_mskor_rtn_b32 %1, %6, %7, %8\n\t"
+                     "ds_mskor_rtn_b32 %2, %9, %10, %11\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2])
+                     : "v"(a[0]), "v"(m[0]), "v"(d[0]), "v"(a[1]), "v"(m[1]), "v"(d[1]), "v"(a[2]), "v"(m[2]),
+                       "v"(d[2]) : "memory");
+    } else {
+        asm volatile("ds_mskor_rtn_b32 %0, %4, %5, %6\n\tds_mskor_rtn_b32 %1, %7, %8, %9\n\t"
+                     "ds_mskor_rtn_b32 %2, %10, %11, %12\n\tds_mskor_rtn_b32 %3, %13, %14, %15\n\t"
+                     "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])
+                     : "v"(a[0]), "v"(m[0]), "v"(d[0]), "v"(a[1]), "v"(m[1]), "v"(d[1]), "v"(a[2]), "v"(m[2]),
+                       "v"(d[2]), "v"(a[3]), "v"(m[3]), "v"(d[3]) : "memory");
+    }
+}
+#endif
+
 template <uint32_t IDB, uint32_t MAXN, uint32_t WIN>
 __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLaneScratch sc)
 {
@@ -480,18 +511,23 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                 uint32_t q1[WIN], cur[WIN];
                 bool need = false;
                 const uint32_t hb = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)H;
+                /* the windows' exchanges in window order, then one wait (the
+                 * results are outputs of the same asm statement) */
+                uint32_t xa[WIN], xm[WIN], xd[WIN], xr[WIN], xs[WIN];
 #pragma unroll
                 for (uint32_t j = 0; j < WIN; j++) {
                     m[j] = ln_mix(ln_slot(tri[j]));
-                    const uint32_t id = m[j] & IDM;
-                    const uint32_t key = ((p[j] + 1u) << IDB) | id;
                     const uint32_t h = act[j] ? (m[j] >> IDB) : BUCKETS + lane;
-                    const uint32_t sh = (h & 1u) << 4;
-                    uint32_t rv;
-                    asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
-                                 : "=&v"(rv)
-                                 : "v"(hb + 4u * (h >> 1)), "v"(0xFFFFu << sh), "v"(key << sh)
-                                 : "memory");
+                    xs[j] = (h & 1u) << 4;
+                    xa[j] = hb + 4u * (h >> 1);
+                    xm[j] = 0xFFFFu << xs[j];
+                    xd[j] = ((((p[j] + 1u) << IDB) | (m[j] & IDM)) & 0xFFFFu) << xs[j];
+                }
+                ks_xchg<WIN>(xr, xa, xm, xd);
+#pragma unroll
+                for (uint32_t j = 0; j < WIN; j++) {
+                    const uint32_t id = m[j] & IDM;
+                    const uint32_t sh = xs[j], rv = xr[j];
                     const uint32_t prev = act[j] ? (rv >> sh) & 0xFFFFu : 0u;
                     const uint32_t ppos = (prev >> IDB) - 1u;            /* prev != 0 */
                     const uint32_t w0 = P + 64u * j;                      /* the window's first position */
