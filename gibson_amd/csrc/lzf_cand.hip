@@ -798,7 +798,16 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
                     cb = p & ~(K3_CB - 1u);
                     d = p - cb;
                     const uint4 *cp = (const uint4 *)(rec + cb);
+#ifdef K3_DUPBLK    /* diagnostic: a second line per record block, same wait */
+                    {
+                        const uint32_t db_ = cb >= 64u ? cb - 64u : cb + 64u;
+                        const uint4 d_ = *(const uint4 *)(rec + db_);
+                        C0 = cp[0];
+                        C0.x |= d_.x & bt.max_len & 0x80000000u;
+                    }
+#else
                     C0 = cp[0];
+#endif
                     C1 = cp[1];
 #if K3_CB == 16
                     C2 = cp[2];
@@ -928,7 +937,17 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
             if (k < lim) {
                 K3_CNT(14);
                 const uint32_t avail = n - (p + k);
-                const uint4 a = dv_ld16_safe(src + p + k, avail), b = dv_ld16_safe(src + q + k, avail);
+                const uint4 a = dv_ld16_safe(src + p + k, avail);
+#ifdef K3_DUPEXT    /* diagnostic: a second line per extension piece's q side, same wait */
+                uint4 b = dv_ld16_safe(src + q + k, avail);
+                {
+                    const uint32_t qd_ = (q + k) >= 256u ? q + k - 256u : q + k + 256u;
+                    const uint4 d_ = dv_ld16(src + (qd_ < n - 16u ? qd_ : 0u));
+                    b.x |= d_.x & bt.max_len & 0x80000000u;
+                }
+#else
+                const uint4 b = dv_ld16_safe(src + q + k, avail);
+#endif
                 W = a;                                   /* literals after the match read it */
                 wb = p + k;
                 const uint32_t d = dv_first_diff(a, b);
