@@ -43,6 +43,7 @@ import gibson_amd  # noqa: E402
 from gibson_amd.shard import reduce_stats, shard  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+RED_DEV = "cpu"         # device of the cross-rank reduction tensors (set in main)
 
 WORKLOADS = {
     # name: (BASELINE config index, synth kind, seed, value bytes, values per GPU)
@@ -192,12 +193,24 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # the ranks meet only at the timing barriers and one reduction of timings
+    # and counts: RCCL by default; LZF_BENCH_BACKEND=gloo does both on the host
+    # (LZF_BENCH_SHARE_GPU=1 puts every rank on device local % count: a
+    # rehearsal of the N-rank path on a one-GPU box, not a measurement)
+    backend = os.environ.get("LZF_BENCH_BACKEND", "nccl")
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        share = os.environ.get("LZF_BENCH_SHARE_GPU") == "1"
+        local_dev = local % torch.cuda.device_count() if share else local
+        torch.cuda.set_device(local_dev)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    global RED_DEV
+    RED_DEV = "cpu" if backend == "gloo" else dev
     if not a.workload:
         a.workload = "text8k" if a.mode == "decompress" else "text64k"
     cfg_idx, kind, seed, n, count = WORKLOADS[a.workload]
@@ -271,7 +284,7 @@ def main():
         good = good and not bool(diff.any())
 
     (wall, t_comp, t_dec), (in_bytes_all, n_ok_all, c_bytes_all, bad_ranks) = reduce_stats(
-        [wall, t_comp, t_dec], [count * n, n_ok, c_bytes, 0 if good else 1], device=dev)
+        [wall, t_comp, t_dec], [count * n, n_ok, c_bytes, 0 if good else 1], device=RED_DEV)
 
     if rank == 0:
         sec_per_step = wall / a.steps
@@ -403,7 +416,7 @@ def main_decompress(a, world, rank, dev, cfg_idx, kind, seed, n, count):
     del src
 
     (wall, t_dec), (n_ok_all, c_bytes_all, bad_ranks) = reduce_stats(
-        [wall, t_dec], [n_ok, c_bytes, 0 if good else 1], device=dev)
+        [wall, t_dec], [n_ok, c_bytes, 0 if good else 1], device=RED_DEV)
     if rank == 0:
         sec_per_step = wall / a.steps
         out_bytes_all = n_ok_all * n
