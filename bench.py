@@ -335,6 +335,8 @@ def main():
                 "algorithmic_bytes": kern[dom][0],
                 "per_kernel_ms": {k: round(v[1] * 1e3, 3) for k, v in kern.items()},
                 "per_kernel_GBps": {k: round(v[0] / v[1] / 1e9, 2) for k, v in kern.items()},
+                # the round trip's read-only fraction, sum(N + C) / t / peak
+                "read_only_frac": round((count * n + c_bytes) / (t_comp + t_dec) / 1e9 / HBM_PEAK_GBPS, 5),
             },
         }
         if world == 1 and not a.no_cpu:
