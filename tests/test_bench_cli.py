@@ -66,3 +66,29 @@ def test_bench_default_is_configs2_with_cpu_baseline():
     cb = line["cpu_baseline"]
     assert cb["cores"] == bench.cpu_cores()[0]
     assert cb["value_1core"] > 0 and cb["value"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [
+    ["--count", "4096"],                                          # weak scaling, round trip
+    ["--workload", "mixed16k", "--total", "8192"],                # strong scaling (configs[4] shape)
+])
+def test_bench_two_ranks_rehearsal(args):
+    # the N-rank path end to end on one GPU: --gpus 2 starts two ranks as a
+    # child torch.distributed.run, both on device 0 (LZF_BENCH_SHARE_GPU),
+    # meeting through gloo; rank 0 prints one line for the whole job
+    import json
+    env = dict(os.environ, LZF_BENCH_BACKEND="gloo", LZF_BENCH_SHARE_GPU="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--warmup", "0", "--no-cpu"] + args,
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-800:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-800:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["roundtrip_ok"] is True
+    assert line["scaling"] == ("strong" if "--total" in args else "weak")
+    if "--total" in args:
+        assert line["config"]["values_per_gpu"] == 4096
