@@ -20,11 +20,14 @@
  *      from a ring Q of q1 over the last 8192 positions (a candidate farther
  *      back is outside every window, src/lzf_c.c:153).  Blocks of 15
  *      windows of 64 positions run through a pipeline (kt_value below):
- *        A  worker wave j takes window j: bytes, slot, and the exact set of
- *           same-slot lanes of the window (16 ballots of the slot bits);
- *        B  the table wave does the T reads and writes of the 15 windows in
- *           order -- one wave's LDS operations execute in order, so T is read
- *           and written in position order without cross-wave ordering;
+ *        A  worker wave j takes window j: bytes and slot;
+ *        B  the table wave exchanges each window's positions into T, window
+ *           by window: ds_mskor_rtn_b32 replaces the slot's 16-bit half and
+ *           returns the old dword, and the LDS runs a wave's same-address
+ *           operations in lane order, so each lane gets the latest earlier
+ *           same-slot position -- the table's or an earlier lane's -- and one
+ *           wave's LDS operations execute in order, so T is updated in
+ *           position order without cross-wave ordering;
  *        C  each worker takes its window again: q1, q2, agreement, record.
  *
  *   2. lzf_parse_rec_kernel -- the greedy parse and emission, ONE LANE PER
@@ -52,26 +55,10 @@
 #ifndef KT_WIN
 #define KT_WIN 15u                /* windows of 64 positions per block = worker waves: 15 + the table wave = 4 per SIMD */
 #endif
-/* same-slot lanes of a window: from three LDS digit bitmaps per worker
- * (KT_BALLOT 0) or from 16 ballots of the slot's bits (1; no LDS) */
-#ifndef KT_BALLOT
-#define KT_BALLOT (KT_WIN > 7u)
-#endif
-/* table step as one lane-ordered 16-bit exchange per window (1; needs 15
- * windows): ds_mskor_rtn_b32 on the dword holding the slot's half returns
- * the latest same-slot position -- the table's or an earlier lane's of the
- * same window -- and leaves the highest lane's, so A computes no same-slot
- * lane masks (tools/lds_mskor_order.hip checks the lane order) */
-#ifndef KT_MSKOR
-#define KT_MSKOR 1
-#endif
 #define KT_BLK (64u * KT_WIN)
 #define KT_THREADS (64u * (KT_WIN + 1u))
 #ifndef KT_PF
 #define KT_PF 4u                /* blocks of input bytes in flight per lane */
-#endif
-#ifndef KT_BF
-#define KT_BF 1                 /* C1/C2 without divergent branches (selects) */
 #endif
 #ifndef KT_CL
 #define KT_CL 2u                /* steps from C1 (agreement loads issued) to C2 (consumed); divides KT_PF */
@@ -83,13 +70,6 @@ __device__ __forceinline__ uint32_t kt_code(uint32_t k)
 }
 
 
-__device__ __forceinline__ void kt_wave_fence()
-{
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-
-#if KT_MSKOR
 static_assert(KT_WIN % 5u == 0u, "the exchanges go in groups of 5 windows");
 /* LDS byte address of a __shared__ object */
 __device__ __forceinline__ uint32_t kt_lds_addr(const void *p)
@@ -111,35 +91,10 @@ __device__ __forceinline__ void kt_xchg5(uint32_t (&r)[5], const uint32_t (&a)[5
                  : KT_IN(0), KT_IN(1), KT_IN(2), KT_IN(3), KT_IN(4)
                  : "memory");
 }
-__device__ __forceinline__ void kt_xchg15(uint32_t (&r)[15], const uint32_t (&a)[15], const uint32_t (&m)[15],
-                                          const uint32_t (&d)[15])
-{
-    asm volatile(KT_X(0) KT_X(1) KT_X(2) KT_X(3) KT_X(4) KT_X(5) KT_X(6) KT_X(7) KT_X(8) KT_X(9) KT_X(10) KT_X(11)
-                     KT_X(12) KT_X(13) KT_X(14) "s_waitcnt lgkmcnt(0)"
-                 : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]),
-                   "=&v"(r[7]), "=&v"(r[8]), "=&v"(r[9]), "=&v"(r[10]), "=&v"(r[11]), "=&v"(r[12]), "=&v"(r[13]),
-                   "=&v"(r[14])
-                 : KT_IN(0), KT_IN(1), KT_IN(2), KT_IN(3), KT_IN(4), KT_IN(5), KT_IN(6), KT_IN(7), KT_IN(8),
-                   KT_IN(9), KT_IN(10), KT_IN(11), KT_IN(12), KT_IN(13), KT_IN(14)
-                 : "memory");
-}
 #undef KT_X
 #undef KT_IN
-#endif
-/* exchanges per asm group (5 or 15) and whether the group's S entries are
- * all read before the first group (1) */
-#ifndef KT_XG
-#define KT_XG 5
-#endif
-#ifndef KT_SHOIST
-#define KT_SHOIST 0
-#endif
-
-/* S entry of a position of the block */
+/* S entry of a position of the block: its slot and whether it is active */
 #define KS_ACT  (1u << 16)
-#define KS_PRED (1u << 17)     /* an earlier lane of its window has its slot */
-#define KS_LAST (1u << 18)     /* no later lane of its window has its slot */
-#define KS_PL   19u            /* bits 19-24: the nearest such earlier lane */
 
 /* the 8 bytes at pp: one branch-free 8-byte load for values of >= 8 bytes
  * (the compiler then counts the loads in flight instead of draining them) */
@@ -165,14 +120,15 @@ __device__ __forceinline__ uint32_t kt_agree(uint2 a, const uint8_t *src, uint32
 /* Pipelined over blocks of KT_BLK = KT_WIN windows (960 positions): wave 0 is
  * the table wave, waves 1..KT_WIN are workers (16 waves: 4 per SIMD), and
  * each step ends with ONE workgroup barrier.  Block k goes through
- *   step k    A(k)   worker j: window j -- bytes, slot, same-slot lanes -> S[k%2]
- *   step k+1  B(k)   table wave: T reads/writes of the windows in order -> O[k%3]
- *   step k+2  C1(k)  worker j: q1, q2 (O[k%3], O[(k-1)%3], Q); agreement loads issued
- *   step k+3  C2(k)  worker j: agreement, record stored; Q <- O[k%3]
+ *   step k         A(k)   worker j: window j -- bytes, slot -> S[k%2]
+ *   step k+1       B(k)   table wave: exchanges of the windows in order -> O[k%3]
+ *   step k+2       C1(k)  worker j: q1, q2 (O[k%3], O[(k-1)%3], Q); agreement loads issued
+ *   step k+3       Q <- O[k%3]
+ *   step k+2+KT_CL C2(k)  worker j: agreement, record stored
  * Q(k) is written in step k+3: the slots it overwrites belong to positions
  * 8192 before block k, which no C1 of block k+1 or later can reach
- * (off < 8192).  The kernel is VALU-bound: the same-slot
- * masks cost 4 VALU per slot bit (v_bfe_i32 + ballot + two v_bitop3). */
+ * (off < 8192).  The kernel is bound by chains of dependent LDS round trips
+ * and the per-step barrier. */
 /* -DKT_TIMING (diagnostic build): cycles per phase, summed over waves in
  * kt_times[]: [0] table wave B, [1] table wave barrier, [2] C2, [3] C1,
  * [4] A, [5] worker loads, [6] worker barrier, [7] steps */
@@ -197,7 +153,6 @@ extern "C" int lzf_gpu_debug_kt(unsigned long long *out16, int reset)
 struct KtLds {
     uint16_t *T, *Q, *O;                 /* O: 3 buffers of KT_BLK */
     uint32_t *S;                         /* S: 2 buffers of KT_BLK */
-    unsigned long long *Dw;              /* this worker's digit bitmaps */
 };
 
 template <uint32_t V> struct KtIc { static constexpr uint32_t value = V; };
@@ -207,14 +162,8 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
 {
     uint16_t *const T = L.T, *const Q = L.Q, *const O = L.O;
     uint32_t *const S = L.S;
-#if !KT_BALLOT
-    unsigned long long *const Dw = L.Dw;
-#endif
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
     const uint32_t j = w - 1u;                                 /* worker's window (w >= 1) */
-    const unsigned long long mine = 1ull << lane, below = mine - 1ull;
-    (void)mine;
-    (void)below;
     const uint32_t np = n - 2u;                                /* positions 0 .. n-3, src/lzf_c.c:145 */
     const uint32_t nb = (np + KT_BLK - 1u) / KT_BLK;
     /* worker: the 8 bytes of its position in the next KT_PF blocks are in
@@ -269,10 +218,8 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
         const uint32_t lp = KT_BLK * (t + KT_PF) + 64u * j + lane;   /* input of block t + KT_PF */
         if (w == 0u) {
             /* ---- B(t-1): the table wave ------------------------------------- */
-            /* no exec masking: every lane reads T[slot] (a read the position
-             * does not need is ignored), a lane that is not its slot's last in
-             * the window writes its own dummy entry T[65536 + lane], and a
-             * lane with an earlier same-slot lane writes O from that lane */
+            /* one lane-ordered exchange per window, in window (= position)
+             * order, five windows per asm group; no exec masking */
 #ifdef KT_ABL_B
             if (false) {
 #else
@@ -281,61 +228,25 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 const uint32_t k = t - 1u, B = KT_BLK * k;
                 const uint32_t *Sk = S + KT_BLK * (k & 1u);
                 uint16_t *Ok = O + KT_BLK * (k % 3u);
-#if KT_MSKOR
                 /* a position past the value exchanges in its lane's own
                  * dummy half (T[65536 + lane]) */
                 const uint32_t tb = kt_lds_addr(T);
-#if KT_SHOIST
-                uint32_t se[KT_WIN];
 #pragma unroll
-                for (uint32_t i = 0; i < KT_WIN; i++) se[i] = Sk[64u * i + lane];
-#endif
+                for (uint32_t g = 0; g < KT_WIN; g += 5u) {
+                    uint32_t xa[5], xm[5], xd[5], xr[5], xs[5];
 #pragma unroll
-                for (uint32_t g = 0; g < KT_WIN; g += KT_XG) {
-                    uint32_t xa[KT_XG], xm[KT_XG], xd[KT_XG], xr[KT_XG], xs[KT_XG];
-#pragma unroll
-                    for (uint32_t u = 0; u < KT_XG; u++) {
+                    for (uint32_t u = 0; u < 5u; u++) {
                         const uint32_t i = g + u;
-#if KT_SHOIST
-                        const uint32_t e = se[i];
-#else
                         const uint32_t e = Sk[64u * i + lane];
-#endif
                         const uint32_t h = (e & KS_ACT) ? (e & 0xFFFFu) : LZF_SLOTS + lane;
                         xs[u] = (h & 1u) << 4;
                         xa[u] = tb + 4u * (h >> 1);
                         xm[u] = 0xFFFFu << xs[u];
                         xd[u] = ((B + 64u * i + lane) & 0xFFFFu) << xs[u];
                     }
-#if KT_XG == 15
-                    kt_xchg15(xr, xa, xm, xd);
-#else
                     kt_xchg5(xr, xa, xm, xd);
-#endif
 #pragma unroll
-                    for (uint32_t u = 0; u < KT_XG; u++) Ok[64u * (g + u) + lane] = (uint16_t)(xr[u] >> xs[u]);
-                }
-                if (false) {
-#else
-                if (true) {
-#endif
-                uint32_t e[KT_WIN], tv[KT_WIN];
-#pragma unroll
-                for (uint32_t i = 0; i < KT_WIN; i++) e[i] = Sk[64u * i + lane];
-#pragma unroll
-                for (uint32_t i = 0; i < KT_WIN; i++) {             /* window order = position order */
-#if defined(KT_ABL_TR) || defined(KT_ABL_TW)
-                    tv[i] = 0u;
-#else
-                    tv[i] = T[e[i] & 0xFFFFu];
-#endif
-#ifndef KT_ABL_TW
-                    T[(e[i] & KS_LAST) ? (e[i] & 0xFFFFu) : LZF_SLOTS + lane] = (uint16_t)(B + 64u * i + lane);
-#endif
-                }
-#pragma unroll
-                for (uint32_t i = 0; i < KT_WIN; i++)
-                    Ok[64u * i + lane] = (uint16_t)((e[i] & KS_PRED) ? B + 64u * i + ((e[i] >> KS_PL) & 63u) : tv[i]);
+                    for (uint32_t u = 0; u < 5u; u++) Ok[64u * (g + u) + lane] = (uint16_t)(xr[u] >> xs[u]);
                 }
             }
         } else {
@@ -343,7 +254,6 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
             if (c_p[CS] < np) {
                 const uint32_t cp = c_p[CS], cq1 = c_q1[CS], cq2 = c_q2[CS], cav = c_avail[CS];
                 const uint2 ca = c_a[CS], cb1 = c_b1[CS], cb2 = c_b2[CS];
-#if KT_BF
                 /* branch-free: both agreements always, the record by selects */
                 const uint64_t x1 = ((uint64_t)(ca.y ^ cb1.y) << 32) | (uint64_t)(ca.x ^ cb1.x);
                 const uint64_t x2 = ((uint64_t)(ca.y ^ cb2.y) << 32) | (uint64_t)(ca.x ^ cb2.x);
@@ -352,22 +262,6 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 const uint32_t r1 = (cp - cq1 - 1u) | (kt_code(k1) << 13);
                 const uint32_t r2 = ((cp - cq2 - 1u) | (kt_code(k2) << 13)) << 16;
                 rec[cp] = cq1 ? (r1 | (cq2 ? r2 : 0u)) : 0u;
-#else
-                uint32_t r = 0u;
-                if (cq1) {
-                    const uint64_t x1 = ((uint64_t)(ca.y ^ cb1.y) << 32) | (uint64_t)(ca.x ^ cb1.x);
-                    uint32_t k1 = x1 ? (uint32_t)__builtin_ctzll(x1) >> 3 : 8u;
-                    k1 = k1 < cav ? k1 : cav;
-                    r = (cp - cq1 - 1u) | (kt_code(k1) << 13);
-                    if (cq2) {
-                        const uint64_t x2 = ((uint64_t)(ca.y ^ cb2.y) << 32) | (uint64_t)(ca.x ^ cb2.x);
-                        uint32_t k2 = x2 ? (uint32_t)__builtin_ctzll(x2) >> 3 : 8u;
-                        k2 = k2 < cav ? k2 : cav;
-                        r |= ((cp - cq2 - 1u) | (kt_code(k2) << 13)) << 16;
-                    }
-                }
-                rec[cp] = r;
-#endif
             }
             /* ---- Q <- O of block t-3 ---------------------------------------- */
             if (t >= 3u && t - 3u < nb) {
@@ -382,7 +276,6 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
             if (t >= 2u && t - 2u < nb) {
                 const uint32_t k = t - 2u, B = KT_BLK * k;
                 const uint32_t p = B + 64u * j + lane;
-#if KT_BF
                 /* branch-free: the Q..O read at a clamped index for every lane,
                  * validity by selects */
                 const bool act = p < np;
@@ -400,25 +293,6 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 c_a[CS] = ak[(PS + KT_PF - 2u) % KT_PF];              /* A's bytes of block t-2 */
                 c_q1[CS] = l1 = q1;
                 c_q2[CS] = l2 = q2;
-#else
-                if (p < np) {
-                    c_p[CS] = p;
-                    const uint16_t *Ok = O + KT_BLK * (k % 3u);
-                    const uint32_t q1 = Ok[64u * j + lane];
-                    c_avail[CS] = n - p;
-                    c_a[CS] = ak[(PS + KT_PF - 2u) % KT_PF];          /* A's bytes of block t-2 */
-                    if (q1 != 0u && p - q1 <= LZF_WINDOW) {          /* off = p - q - 1 < 8192 */
-                        /* Ok / Op / the ring, as one index into Q..O */
-                        const uint32_t ik = LZF_WINDOW + KT_BLK * (k % 3u), ip = LZF_WINDOW + KT_BLK * ((k + 2u) % 3u);
-                        const uint32_t iq = q1 >= B ? ik + (q1 - B)
-                                          : q1 + KT_BLK >= B ? ip + (q1 + KT_BLK - B)
-                                                             : (q1 & (LZF_WINDOW - 1u));
-                        const uint32_t q2 = Q[iq];
-                        c_q1[CS] = l1 = q1;
-                        if (q2 != 0u && p - q2 <= LZF_WINDOW) c_q2[CS] = l2 = q2;
-                    }
-                }
-#endif
             }
             KT_TM(3);
             /* ---- A(t): the worker's window of block t ----------------------- */
@@ -428,47 +302,7 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 const uint2 a = pf[PS];
                 ak[PS] = a;
                 const uint32_t s = dv_slot(a.x);
-#if KT_MSKOR
                 S[KT_BLK * (t & 1u) + 64u * j + lane] = act ? (s | KS_ACT) : 0u;
-#else
-#if KT_BALLOT
-                /* exact: the lanes agreeing with mine on every slot bit.  Per
-                 * bit: x = my bit sign-extended (0 / ~0), its ballot bb, and
-                 * M &= ~(bb ^ x) as one v_bitop3 per half (4 VALU per bit) */
-                const unsigned long long M0 = __ballot(act);
-                uint32_t mlo = (uint32_t)M0, mhi = (uint32_t)(M0 >> 32);
-#pragma unroll
-                for (uint32_t b = 0; b < 16u; b++) {
-                    uint32_t x;                          /* v_bfe_i32: the compiler would split it */
-                    asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(x) : "v"(s), "n"(b));
-                    const unsigned long long bb = __ballot(x != 0u);
-                    mlo = __builtin_amdgcn_bitop3_b32(mlo, (uint32_t)bb, x, 0x90);
-                    mhi = __builtin_amdgcn_bitop3_b32(mhi, (uint32_t)(bb >> 32), x, 0x90);
-                }
-                unsigned long long M = ((unsigned long long)mhi << 32) | mlo;
-                if (!act) M = 0ull;
-#else
-                const uint32_t i0 = s & 63u, i1 = 64u + ((s >> 6) & 63u), i2 = 128u + (s >> 12);
-                if (act) {
-                    __hip_atomic_fetch_or(&Dw[i0], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_or(&Dw[i1], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_or(&Dw[i2], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-                kt_wave_fence();
-                const unsigned long long M = act ? (Dw[i0] & Dw[i1] & Dw[i2]) : 0ull;   /* same-slot lanes */
-                kt_wave_fence();
-                if (act) {
-                    Dw[i0] = 0ull;
-                    Dw[i1] = 0ull;
-                    Dw[i2] = 0ull;
-                }
-#endif
-                const unsigned long long pb = M & below;
-                const uint32_t pl = pb ? 63u - (uint32_t)__builtin_clzll(pb) : 0u;
-                S[KT_BLK * (t & 1u) + 64u * j + lane] =
-                    act ? (s | KS_ACT | (pb ? KS_PRED : 0u) | ((M >> lane) == 1ull ? KS_LAST : 0u) | (pl << KS_PL))
-                        : 0u;
-#endif
             }
         }
         if (w) KT_TM(4);
@@ -524,22 +358,9 @@ __global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt,
     __shared__ uint16_t QO[LZF_WINDOW + 3u * KT_BLK];
     uint16_t *const Q = QO, *const O = QO + LZF_WINDOW;
     __shared__ uint32_t S[2u * KT_BLK];
-#if KT_BALLOT
-    unsigned long long *const Dw = nullptr;
-#else
-    __shared__ unsigned long long D[KT_WIN][144];                      /* slot digit bitmaps per worker */
-#endif
-#if !KT_BALLOT
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    unsigned long long *const Dw = D[w ? w - 1u : 0u];
-#endif
-    const KtLds L{T, Q, O, S, Dw};
+    const KtLds L{T, Q, O, S};
 #ifdef KT_PRIO
     if (threadIdx.x < 64u) __builtin_amdgcn_s_setprio(KT_PRIO);   /* the table wave */
-#endif
-#if !KT_BALLOT
-    if (w)
-        for (uint32_t k = lane; k < 144u; k += 64u) Dw[k] = 0ull;
 #endif
     for (uint32_t v = blockIdx.x; v < bt.count; v += gridDim.x) {
         const uint32_t n = bt.in_len[v];
