@@ -289,11 +289,6 @@ hipError_t lzf_launch_decompress_lane(const LzfBatch &b, hipStream_t s)
 #ifndef KS8_WIN
 #define KS8_WIN     2u            /* 8 KiB small class: windows per step */
 #endif
-/* small class: bucket heads by a lane-ordered exchange (1) instead of the
- * digit lane bitmaps (0) */
-#ifndef KS_XCHG
-#define KS_XCHG     1
-#endif
 #define KS_MAXN     4096u         /* small class: 12-bit bucket, 4-bit identity, positions + 1 fit 12 bits */
 #define KS8_MAXN    8192u         /* small class, 8 KiB: 13-bit bucket, 3-bit identity, positions + 1 fit 13 bits */
 #define KM_BUCKETS  2048u         /* mid class */
@@ -376,17 +371,16 @@ __device__ __noinline__ void k1_fix_order(uint32_t (&r)[K1_WIN], const uint32_t 
  * Slot-mix m = mix(slot) (bijective): bucket = m >> IDB, identity = the low
  * IDB bits (IDB = 4 for values <= 4 KiB, 3 for values <= 8 KiB, so that an
  * entry [pos+1 | identity] fits 16 bits).
- * Per window of 64 positions, lanes with the same bucket / the same slot are
- * found exactly with lane bitmaps keyed by m's digits [IDB,IDB+6),
- * [IDB+6,16) and [0,IDB) (ds_or_b64, AND of the read-backs).  Per position the kernel keeps,
- * in LDS, the bucket head (latest position of the bucket) and a skip link:
- * the latest earlier position of the bucket with ANOTHER identity.  The
- * same-slot predecessor is then the nearest same-slot lane below, else found
- * from the head by following skip links until the identity matches (one hop
- * per change of identity, not per position).  Entries are [pos+1:16-IDB |
- * identity:IDB].  LDS at 4 KiB: heads 8 KiB, links 8 KiB, bytes 4 KiB,
- * bitmaps 1.1 KiB per window; at 8 KiB: heads 16 KiB, links 16 KiB, bytes
- * 8 KiB, bitmaps 1.6 KiB per window. */
+ * Per position the kernel keeps, in LDS, the bucket head (latest position of
+ * the bucket) and a skip link: the latest earlier position of the bucket
+ * with ANOTHER identity.  Per window of 64 positions one lane-ordered 16-bit
+ * exchange on the heads (ds_mskor_rtn_b32) gives each lane its latest
+ * earlier same-bucket position, the head's or an earlier lane's; the
+ * same-slot predecessor follows the skip links from there until the
+ * identity matches (one hop per change of identity, not per position).
+ * Entries are [pos+1:16-IDB | identity:IDB].  LDS at 4 KiB: heads 8 KiB,
+ * links 8 KiB, bytes 4 KiB; at 8 KiB: heads 16 KiB, links 16 KiB, bytes
+ * 8 KiB. */
 __device__ __forceinline__ uint32_t ks_rd4(const uint32_t *w, uint32_t x)
 {
     return __builtin_amdgcn_alignbyte(w[(x >> 2) + 1u], w[x >> 2], x & 3u);
@@ -398,7 +392,6 @@ __device__ __forceinline__ uint32_t ks_hibit(uint64_t m)
     return 63u - (uint32_t)__builtin_clzll(m);
 }
 
-#if KS_XCHG
 /* WIN lane-ordered 16-bit exchanges (ds_mskor_rtn_b32), issued in order, one wait */
 template <uint32_t WIN>
 __device__ __forceinline__ void ks_xchg(uint32_t (&r)[WIN], const uint32_t (&a)[WIN], const uint32_t (&m)[WIN],
@@ -427,36 +420,19 @@ __device__ __forceinline__ void ks_xchg(uint32_t (&r)[WIN], const uint32_t (&a)[
                        "v"(d[2]), "v"(a[3]), "v"(m[3]), "v"(d[3]) : "memory");
     }
 }
-#endif
 
 template <uint32_t IDB, uint32_t MAXN, uint32_t WIN>
 __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLaneScratch sc)
 {
     static_assert(MAXN <= LZF_WINDOW && ((MAXN - 1u) >> (16u - IDB)) == 0u, "entry [pos+1 | id] must fit 16 bits");
     constexpr uint32_t BUCKETS = 1u << (16u - IDB), IDM = (1u << IDB) - 1u;
-    constexpr uint32_t T0 = 0u;                          /* digit m[IDB, IDB+6)  : 64 entries */
-    constexpr uint32_t T1 = 64u;                         /* digit m[IDB+6, 16)   : 2^(10-IDB) entries */
-    constexpr uint32_t T2 = T1 + (1u << (10u - IDB));    /* digit m[0, IDB)      : 2^IDB entries */
-    constexpr uint32_t TN = T2 + (1u << IDB);
     constexpr uint32_t PF = MAXN / 1024u;                /* 16-byte loads per lane per value */
-    __shared__ __attribute__((aligned(16))) uint16_t H[BUCKETS + 64u];   /* + one dummy per lane (KS_XCHG) */
+    __shared__ __attribute__((aligned(16))) uint16_t H[BUCKETS + 64u];   /* + one dummy per lane */
     __shared__ uint16_t E[MAXN];
     __shared__ __attribute__((aligned(16))) uint32_t Bw[MAXN / 4u + 4u];
-#if !KS_XCHG
-    __shared__ unsigned long long T[WIN][TN];
-#endif
     const uint32_t lane = threadIdx.x;
-    const unsigned long long mine = 1ull << lane, below = mine - 1ull;
     uint32_t v = blockIdx.x;
     if (v >= bt.count) return;
-#if KS_XCHG
-    (void)mine;
-    (void)below;
-    (void)T0;
-    (void)TN;
-#else
-    for (uint32_t k = lane; k < WIN * TN; k += 64u) (&T[0][0])[k] = 0ull;
-#endif
     uint4 pf[PF];
     uint32_t pn = bt.in_len[v];
     {
@@ -496,7 +472,6 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                     act[j] = p[j] < np;
                     tri[j] = ks_rd4(Bw, act[j] ? p[j] : 0u);
                 }
-#if KS_XCHG
                 /* one lane-ordered 16-bit exchange per window on the bucket's
                  * head (ds_mskor_rtn_b32, tools/lds_mskor_order.hip): each lane
                  * gets the latest earlier position of its bucket -- the
@@ -547,70 +522,6 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                     if (cur[j] && (cur[j] & IDM) == id) { q1[j] = cur[j] >> IDB; cur[j] = 0u; }
                     need |= cur[j] != 0u;
                 }
-#else
-#pragma unroll
-                for (uint32_t j = 0; j < WIN; j++) {
-                    m[j] = ln_mix(ln_slot(tri[j]));
-#ifndef KS_ABL_T
-                    if (act[j]) {
-                        __hip_atomic_fetch_or(&T[j][T0 + ((m[j] >> IDB) & 63u)], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_or(&T[j][T1 + (m[j] >> (IDB + 6u))], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_or(&T[j][T2 + (m[j] & IDM)], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-#endif
-                }
-                ln_wave_fence();
-                unsigned long long MB[WIN], MS[WIN];
-#pragma unroll
-                for (uint32_t j = 0; j < WIN; j++) {
-#ifdef KS_ABL_T
-                    MB[j] = MS[j] = mine;
-#else
-                    MB[j] = T[j][T0 + ((m[j] >> IDB) & 63u)] & T[j][T1 + (m[j] >> (IDB + 6u))];
-                    MS[j] = MB[j] & T[j][T2 + (m[j] & IDM)];
-#endif
-                    if (!act[j]) MB[j] = MS[j] = 0ull;
-                }
-                ln_wave_fence();
-#pragma unroll
-                for (uint32_t j = 0; j < WIN; j++) {
-#ifndef KS_ABL_T
-                    if (act[j]) {
-                        T[j][T0 + ((m[j] >> IDB) & 63u)] = 0ull;
-                        T[j][T1 + (m[j] >> (IDB + 6u))] = 0ull;
-                        T[j][T2 + (m[j] & IDM)] = 0ull;
-                    }
-#endif
-                }
-                /* window j reads the heads after window j-1 wrote them (LDS
-                 * ops of a wave execute in order) */
-                uint32_t q1[WIN], cur[WIN];
-                bool need = false;
-#pragma unroll
-                for (uint32_t j = 0; j < WIN; j++) {
-                    const uint32_t bk = m[j] >> IDB, id = m[j] & IDM;
-                    const uint32_t key = ((p[j] + 1u) << IDB) | id;
-                    const unsigned long long ss = MS[j] & below, sb = MB[j] & ~MS[j] & below;
-                    const uint32_t h = act[j] ? (uint32_t)H[bk] : 0u;
-                    const uint32_t eh = (act[j] && h) ? (uint32_t)E[(h >> IDB) - 1u] : 0u;
-                    /* skip link: latest earlier bucket position with another identity */
-                    const uint32_t lsb = sb ? ks_hibit(sb) : lane;
-                    const uint32_t ksb = (uint32_t)__shfl((int)key, (int)lsb);
-                    const uint32_t link = sb ? ksb : ((h & IDM) != id ? h : eh);
-                    if (act[j]) E[p[j]] = (uint16_t)link;
-                    if (act[j] && (MB[j] >> lane) == 1ull) H[bk] = (uint16_t)key;
-                    /* same-slot predecessor */
-                    q1[j] = ss ? P + 64u * j + ks_hibit(ss) + 1u : 0u;    /* pos+1 */
-                    cur[j] = (act[j] && !ss) ? h : 0u;
-                    if (cur[j] && (cur[j] & IDM) == id) { q1[j] = cur[j] >> IDB; cur[j] = 0u; }
-                    /* the head's own link is eh, read above: the first hop is free */
-                    if (cur[j]) {
-                        cur[j] = eh;
-                        if (eh && (eh & IDM) == id) { q1[j] = eh >> IDB; cur[j] = 0u; }
-                    }
-                    need |= cur[j] != 0u;
-                }
-#endif /* KS_XCHG */
                 ln_wave_fence();
 #ifdef KS_ABL_WALK
                 need = false;
