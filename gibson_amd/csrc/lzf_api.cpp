@@ -4,10 +4,11 @@
  * Exports the drop-in pair of include/lzf.h (replacing src/lzf_c.c:98 and
  * src/lzf_d.c:55 behind the prototypes of src/lzf.h:76-78, 95-97) and the
  * batched device API of include/lzf_gpu.h.  There is no CPU codec in this
- * library: every call runs the HIP kernels; when no gfx950 device is
- * usable the single-call entry points abort with a message (a GPU-backed
- * codec without a GPU is a deployment error, not a silent fallback) and the
- * batch calls return LZF_GPU_ENODEV.
+ * library: every call runs the HIP kernels.  Failures never abort (a server
+ * must survive a transient HIP error): when no gfx950 device is usable or a
+ * HIP call fails, lzf_compress returns 0 (the caller stores the value plain,
+ * src/query.c:393), lzf_decompress returns 0 with errno EIO, and the batch
+ * calls return a negative LZF_GPU_E* code (LZF_GPU_ENODEV without a device).
  *
  * Single calls are batches of one.  Each calling thread owns a context
  * (stream, device buffers, pinned staging), created lazily on the device
@@ -35,7 +36,7 @@ hipError_t lzf_launch_decompress_serial(const LzfBatch &b, hipStream_t s);
 
 namespace {
 
-enum KernelGen { GEN_TABLE = 0, GEN_LANE = 1, GEN_WINDOW = 2, GEN_SERIAL = 3 };
+enum KernelGen { GEN_TABLE = 0, GEN_LANE = 1, GEN_WINDOW = 2, GEN_SERIAL = 3, GEN_WTAB = 4 };
 
 /* LZF_GPU_KERNEL picks the kernel generation, read per launch so one process
  * can A/B them.  Unset: the measured routing of launch_compress (the table
@@ -52,6 +53,7 @@ KernelGen kernel_gen()
 #endif
     if (e && !strcmp(e, "window")) return GEN_WINDOW;
     if (e && !strcmp(e, "lane")) return GEN_LANE;
+    if (e && !strcmp(e, "wtab")) return GEN_WTAB;
     return GEN_TABLE;
 }
 
@@ -126,14 +128,20 @@ void scratch_free(Scratch &S)
     S.used = false;
 }
 
-hipError_t lane_compress(const LzfBatch &b, hipStream_t s, bool table)
+enum ScratchUser { SU_LANE = 0, SU_TABLE = 1, SU_WTAB = 2 };
+uint32_t g_last_chunks = 0;          /* chunks of the last scratch-bound compress launch */
+
+hipError_t lane_compress(const LzfBatch &b, hipStream_t s, ScratchUser who)
 {
+    const bool table = who == SU_TABLE;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     Scratch &S = g_scratch[dev & 63];
     std::lock_guard<std::mutex> lk(S.mu);
-    const size_t per = table ? lzf_table_scratch_per_value(b.max_len) : lzf_lane_scratch_per_value(b.max_len);
+    const size_t per = who == SU_WTAB ? lzf_wtab_scratch_per_value(b.max_len)
+                       : table        ? lzf_table_scratch_per_value(b.max_len)
+                                      : lzf_lane_scratch_per_value(b.max_len);
     size_t want = per * (size_t)b.count + 512;
     const size_t lim = scratch_limit(S.cap);
     if (want > lim) want = lim;
@@ -154,7 +162,9 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s, bool table)
     }
     if (!S.ev && (e = hipEventCreateWithFlags(&S.ev, hipEventDisableTiming)) != hipSuccess) return e;
     if (S.used && S.last != s && (e = hipStreamWaitEvent(s, S.ev, 0)) != hipSuccess) return e;
-    if (table) {
+    if (who == SU_WTAB) {
+        e = lzf_launch_compress_wtab(b, s, S.p, S.cap, &g_last_chunks);
+    } else if (table) {
         e = lzf_launch_compress_table(b, s, S.p, S.cap);
     } else {
 #ifdef LZF_DIAG
@@ -208,8 +218,10 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
     case GEN_WINDOW: return lzf_launch_compress(b, s);
     case GEN_LANE:
         return (lzf_lane_compress_supported(b.max_len) && b.count >= lane_min_count(b.max_len))
-                   ? lane_compress(b, s, false)
+                   ? lane_compress(b, s, SU_LANE)
                    : lzf_launch_compress(b, s);
+    case GEN_WTAB:
+        return lzf_wtab_compress_supported(b.max_len) ? lane_compress(b, s, SU_WTAB) : lzf_launch_compress(b, s);
     default:
         /* batches with values past 64 KiB, and small batches, go to the window
          * generation: the parse runs one value per lane, so its time has a
@@ -221,7 +233,7 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
          * text64k 262 vs 485 ms; profiles/r02/workloads.txt) */
         if (b.count < lane_min_count(b.max_len) || !lzf_table_compress_supported(b.max_len))
             return lzf_launch_compress(b, s);
-        return lane_compress(b, s, b.max_len > 4096u);
+        return lane_compress(b, s, b.max_len > 4096u ? SU_TABLE : SU_LANE);
     }
 }
 
@@ -784,6 +796,10 @@ const char *lzf_gpu_kernel_info(void)
     case GEN_WINDOW:
         s = std::string("compress=") + lzf_compress_kernel_name() + " decompress=" +
             lzf_decompress_kernel_name();
+        break;
+    case GEN_WTAB:
+        s = std::string("compress=wtab(cand_q1+wparse; window64 past 64 KiB) decompress=") +
+            lzf_decompress_kernel_name() + " scratch_chunks=" + std::to_string(g_last_chunks);
         break;
     case GEN_LANE:
         s = std::string("compress=lane(cand+parse; window64 past 64 KiB or below ") +

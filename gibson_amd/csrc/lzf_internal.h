@@ -76,6 +76,10 @@ struct LzfRecScratch {
 hipError_t lzf_launch_compress_table(const LzfBatch &b, hipStream_t s, void *scratch, size_t scratch_bytes);
 size_t lzf_table_scratch_per_value(uint32_t max_len);
 bool lzf_table_compress_supported(uint32_t max_len);
+hipError_t lzf_launch_compress_wtab(const LzfBatch &b, hipStream_t s, void *scratch, size_t scratch_bytes,
+                                    uint32_t *chunks);
+size_t lzf_wtab_scratch_per_value(uint32_t max_len);
+bool lzf_wtab_compress_supported(uint32_t max_len);
 hipError_t lzf_launch_decompress_lane(const LzfBatch &b, hipStream_t s);
 /* aux / ev (4 events) optional: chunks pipelined over s (kernel 1) and aux
  * (kernel 2); s is joined with aux before returning */

@@ -18,7 +18,7 @@ from tests.oracle_lib import sha16, synth
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-GENERATIONS = ["table", "lane", "window", "serial", "lane-diag"]
+GENERATIONS = ["table", "wtab", "lane", "window", "serial", "lane-diag"]
 DIAG = {"serial", "lane-diag"}      # cross-check forms: the diagnostic build only
 
 
@@ -409,9 +409,19 @@ def digests():
 
 @pytest.mark.parametrize("kind,seed,n,count", CONFIGS)
 def test_full_batch_digest_and_roundtrip(kind, seed, n, count, digests, monkeypatch):
+    monkeypatch.delenv("LZF_GPU_LANE_MIN", raising=False)      # the routing the bench uses
+    _digest_case(kind, seed, n, count, digests)
+
+
+@pytest.mark.parametrize("kind,seed,n,count", [c for c in CONFIGS if c[3] <= 65536])
+def test_full_batch_digest_wtab(kind, seed, n, count, digests, monkeypatch):
+    monkeypatch.setenv("LZF_GPU_KERNEL", "wtab")
+    _digest_case(kind, seed, n, count, digests)
+
+
+def _digest_case(kind, seed, n, count, digests):
     import gibson_amd
     from tests.digest import batch_digest
-    monkeypatch.delenv("LZF_GPU_LANE_MIN", raising=False)      # the routing the bench uses
     dev = "cuda"
     src = torch.empty(count * n, dtype=torch.uint8, device=dev)
     gibson_amd.synth_fill(kind, seed, 0, 1, count, n, src)
