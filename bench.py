@@ -43,6 +43,7 @@ import gibson_amd  # noqa: E402
 from gibson_amd.shard import reduce_stats, shard  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+CHUNK_BYTES = 16 << 30  # codec chunk of a batch past this many input bytes
 RED_DEV = "cpu"         # device of the cross-rank reduction tensors (set in main)
 
 WORKLOADS = {
@@ -219,51 +220,79 @@ def main():
     if a.count:
         count = a.count
     if a.total:                                          # strong scaling: rank's round-robin share
+        if a.total < world:
+            sys.exit(f"bench.py: --total {a.total} gives rank {world - 1} no value (fewer values than ranks)")
         count = (a.total - rank + world - 1) // world
     if a.mode == "decompress":
         return main_decompress(a, world, rank, dev, cfg_idx, kind, seed, n, count)
 
     # ---- data in HBM: value i of this rank is global value rank + k*world ----
+    # A batch past CHUNK_BYTES (BASELINE configs[4] at N = 1: 4 M x 16 KiB =
+    # 64 GiB) keeps every input and stream resident but runs the codec in
+    # chunks of <= 16 GiB (SURVEY.md §8(d) timing rules): the kernels' scratch
+    # and the decode arena are per chunk; a step is all chunks in order.
+    chunk = count if count * n <= CHUNK_BYTES else max(1, CHUNK_BYTES // n)
+    nch = (count + chunk - 1) // chunk
     src = torch.empty(count * n, dtype=torch.uint8, device=dev)
     first, stride = shard(rank, world)
     gibson_amd.synth_fill(kind, seed, first, stride, count, n, src)
-    off = torch.arange(count, dtype=torch.int64, device=dev) * n
-    in_len = torch.full((count,), n, dtype=torch.int32, device=dev)
-    ccap = torch.full((count,), n - 4, dtype=torch.int32, device=dev)
+    off = torch.arange(chunk, dtype=torch.int64, device=dev) * n
+    in_len = torch.full((chunk,), n, dtype=torch.int32, device=dev)
+    ccap = torch.full((chunk,), n - 4, dtype=torch.int32, device=dev)
     comp = torch.empty(count * n, dtype=torch.uint8, device=dev)
     clen = torch.zeros(count, dtype=torch.int32, device=dev)
-    dcap = torch.full((count,), n, dtype=torch.int32, device=dev)
-    dec = torch.empty(count * n, dtype=torch.uint8, device=dev)
-    dlen = torch.zeros(count, dtype=torch.int32, device=dev)
-    derr = torch.zeros(count, dtype=torch.int32, device=dev)
+    dcap = torch.full((chunk,), n, dtype=torch.int32, device=dev)
+    dec = torch.empty(chunk * n, dtype=torch.uint8, device=dev)
+    dlen = torch.zeros(chunk, dtype=torch.int32, device=dev)
+    derr = torch.zeros(chunk, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream()
     torch.cuda.synchronize()
 
     ev = []
+    good = True
 
-    def step(record):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e2 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        gibson_amd.compress_batch(src, off, in_len, comp, off, ccap, clen, n, stream)
-        e1.record(stream)
-        # failed values (clen == 0) decode a 0-length stream: one control byte
-        # and an immediate error, i.e. they are skipped as in the server
-        gibson_amd.decompress_batch(comp, off, clen, dec, off, dcap, dlen, derr, n, stream)
-        e2.record(stream)
-        if record:
-            ev.append((e0, e1, e2))
+    def verify(c0, m):
+        """every compressed value of chunk [c0, c0 + m) decoded back (untimed)"""
+        ok = clen[c0:c0 + m] > 0
+        g = bool(((dlen[:m] == n) | ~ok).all())
+        dv, sv = dec[:m * n].view(m, n), src[c0 * n:(c0 + m) * n].view(m, n)
+        for r0 in range(0, m, 1 << 16):
+            r1 = min(m, r0 + (1 << 16))
+            g = g and not bool(((dv[r0:r1] != sv[r0:r1]).any(dim=1) & ok[r0:r1]).any())
+        return g
 
-    for _ in range(a.warmup):
-        step(False)
+    def step(record, check):
+        nonlocal good
+        for ci in range(nch):
+            c0 = ci * chunk
+            m = min(chunk, count - c0)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e2 = torch.cuda.Event(enable_timing=True)
+            sv, cv = src[c0 * n:(c0 + m) * n], comp[c0 * n:(c0 + m) * n]
+            e0.record(stream)
+            gibson_amd.compress_batch(sv, off[:m], in_len[:m], cv, off[:m], ccap[:m], clen[c0:c0 + m], n, stream)
+            e1.record(stream)
+            # failed values (clen == 0) decode a 0-length stream: one control
+            # byte and an immediate error, i.e. they are skipped as in the server
+            gibson_amd.decompress_batch(cv, off[:m], clen[c0:c0 + m], dec, off[:m], dcap[:m], dlen[:m], derr[:m],
+                                        n, stream)
+            e2.record(stream)
+            if record:
+                ev.append((e0, e1, e2))
+            if check:
+                torch.cuda.synchronize()
+                good = verify(c0, m) and good
+
+    for w_ in range(a.warmup):
+        step(False, w_ == 0)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        step(True)
+        step(True, False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -275,13 +304,10 @@ def main():
     ok = clen > 0
     n_ok = int(ok.sum())
     c_bytes = int(clen.to(torch.int64).sum())
-    # sanity (outside the timed region): every compressed value decoded back
-    good = bool(((dlen == n) | ~ok).all())
-    dv, sv = dec.view(count, n), src.view(count, n)
-    for r0 in range(0, count, 1 << 16):
-        r1 = min(count, r0 + (1 << 16))
-        diff = (dv[r0:r1] != sv[r0:r1]).any(dim=1) & ok[r0:r1]
-        good = good and not bool(diff.any())
+    # sanity (outside the timed region): the last chunk of the last step, and
+    # every chunk in the first warm-up step
+    c0 = (nch - 1) * chunk
+    good = verify(c0, count - c0) and good
 
     (wall, t_comp, t_dec), (in_bytes_all, n_ok_all, c_bytes_all, bad_ranks) = reduce_stats(
         [wall, t_comp, t_dec], [count * n, n_ok, c_bytes, 0 if good else 1], device=RED_DEV)
@@ -323,6 +349,8 @@ def main():
                 "ratio": round(c_bytes_all / max(1.0, n_ok_all * n), 4),
                 "kernels": gibson_amd.kernel_info(),
                 "roundtrip_ok": bad_ranks == 0,
+                "chunks": nch,
+                "chunk_values": chunk,
             },
             "roofline": {
                 "bound": "hbm",
@@ -450,6 +478,8 @@ def main_decompress(a, world, rank, dev, cfg_idx, kind, seed, n, count):
                 "ratio": round(c_bytes_all / max(1.0, out_bytes_all), 4),
                 "kernels": gibson_amd.kernel_info(),
                 "roundtrip_ok": bad_ranks == 0,
+                "chunks": nch,
+                "chunk_values": chunk,
             },
             "roofline": {
                 "bound": "hbm",

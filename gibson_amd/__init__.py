@@ -17,6 +17,9 @@ from .lzf import (  # noqa: F401
     LzfLibraryMissing,
     compress_batch,
     decompress_batch,
+    decoded_size_batch,
+    lds_order_probe,
+    selfcheck,
     kernel_info,
     release,
     lib,

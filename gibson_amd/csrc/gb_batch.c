@@ -123,6 +123,10 @@ static int gb_put(uint8_t **p, uint64_t *space, const void *src, uint64_t n)
     return 0;
 }
 
+/* bytes of the decode arena of the calling thread's last gb_mget_payload */
+static _Thread_local uint64_t g_mget_staged;
+uint64_t gb_mget_last_staged(void) { return g_mget_staged; }
+
 long gb_mget_payload(const uint8_t *keys, const uint64_t *key_off, const uint32_t *key_len,
                      const uint8_t *vals, const uint64_t *val_off, const uint32_t *val_size,
                      const uint8_t *enc, const uint32_t *orig_len, uint32_t count, uint32_t elements,
@@ -130,20 +134,20 @@ long gb_mget_payload(const uint8_t *keys, const uint64_t *key_off, const uint32_
 {
     if (!out || (count && (!keys || !key_off || !key_len || !vals || !val_off || !val_size || !enc)))
         return LZF_GPU_EARG;
-    /* one decode batch for every LZF item, output caps from the side table
-     * (maxrequestsize where the original length is unknown) */
+    g_mget_staged = 0;
+    /* One decode batch for the LZF items, each into a slot of its decoded
+     * size.  The reference decodes with out_len = maxrequestsize
+     * (src/net.c:1309-1315): a side-table length caps at that, and an item
+     * with no entry is sized first by the device pre-pass
+     * (lzf_host_decoded_size_batch) at that out_len -- no slot of
+     * maxrequestsize bytes per item. */
     uint32_t m = 0;
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < count; i++) {
-        if (enc[i] != GB_ENC_LZF) continue;
-        const uint32_t c = (orig_len && orig_len[i]) ? orig_len[i] : maxrequestsize;
-        total += c;
-        m++;
-    }
-    uint32_t *len = NULL, *cap = NULL, *dl = NULL;
+    for (uint32_t i = 0; i < count; i++)
+        if (enc[i] == GB_ENC_LZF) m++;
+    uint32_t *len = NULL, *cap = NULL, *dl = NULL, *ul = NULL, *us = NULL;
     int32_t *er = NULL;
-    uint64_t *ioff = NULL, *ooff = NULL, *pos = NULL;
-    uint8_t *dec = NULL;
+    uint64_t *ioff = NULL, *ooff = NULL, *pos = NULL, *uo = NULL;
+    uint8_t *dec = NULL, *exact = NULL;
     long ret = 0;
     if (m) {
         len = malloc(m * sizeof *len);
@@ -152,27 +156,96 @@ long gb_mget_payload(const uint8_t *keys, const uint64_t *key_off, const uint32_
         er = malloc(m * sizeof *er);
         ioff = malloc(m * sizeof *ioff);
         ooff = malloc(m * sizeof *ooff);
+        exact = malloc(m);
         pos = malloc(count * sizeof *pos);
-        dec = malloc(total ? total : 1);
-        if (!len || !cap || !dl || !er || !ioff || !ooff || !pos || !dec) {
+        uo = malloc(m * sizeof *uo);
+        ul = malloc(m * sizeof *ul);
+        us = malloc(m * sizeof *us);
+        if (!len || !cap || !dl || !er || !ioff || !ooff || !exact || !pos || !uo || !ul || !us) {
             ret = LZF_GPU_ENOMEM;
             goto done;
         }
-        uint64_t o = 0;
+        uint32_t nu = 0;
         for (uint32_t i = 0, k = 0; i < count; i++) {
             if (enc[i] != GB_ENC_LZF) continue;
             ioff[k] = val_off[i];
             len[k] = val_size[i];
-            cap[k] = (orig_len && orig_len[i]) ? orig_len[i] : maxrequestsize;
-            ooff[k] = o;
             pos[i] = k;
-            o += cap[k];
+            if (orig_len && orig_len[i]) {
+                cap[k] = orig_len[i] < maxrequestsize ? orig_len[i] : maxrequestsize;
+                exact[k] = 0;
+            } else {
+                uo[nu] = val_off[i];
+                ul[nu] = val_size[i];
+                nu++;
+                cap[k] = 0;
+                exact[k] = 1;
+            }
             k++;
         }
-        const int rc = lzf_host_decompress_batch(vals, ioff, len, dec, ooff, cap, dl, er, m);
+        if (nu) {
+            const int rc = lzf_host_decoded_size_batch(vals, uo, ul, us, er, nu, maxrequestsize);
+            if (rc) {
+                ret = rc;
+                goto done;
+            }
+            for (uint32_t k = 0, u = 0; k < m; k++)
+                if (exact[k]) cap[k] = us[u++];                   /* 0: the item does not decode */
+        }
+        /* when every size is exact, a payload past max_response fails the
+         * reference's CHECK_SPACE (src/net.c:1272-1277) whatever the order:
+         * nothing is decoded then */
+        {
+            uint64_t need = 4;
+            int all_exact = 1;
+            for (uint32_t i = 0; i < count; i++) {
+                if (enc[i] == GB_ENC_NULL) continue;
+                uint64_t v = val_size[i];
+                if (enc[i] == GB_ENC_LZF) {
+                    v = cap[pos[i]];
+                    all_exact &= exact[pos[i]];
+                }
+                need += 4u + (uint64_t)key_len[i] + 1u + 4u + v;
+            }
+            if (all_exact && need > max_response) goto done;
+        }
+        uint64_t total = 0;
+        for (uint32_t k = 0; k < m; k++) {
+            ooff[k] = total;
+            total += cap[k];
+        }
+        dec = malloc(total ? total : 1);
+        if (!dec) {
+            ret = LZF_GPU_ENOMEM;
+            goto done;
+        }
+        g_mget_staged = total;
+        for (uint32_t k = 0; k < m; k++) dl[k] = 0;
+        /* an item of size 0 (does not decode) keeps cap 0: it fails again
+         * in the batch, and the frame below stops there as the reference does */
+        int rc = lzf_host_decompress_batch(vals, ioff, len, dec, ooff, cap, dl, er, m);
         if (rc) {
             ret = rc;
             goto done;
+        }
+        /* a side-table length that was too small (stale): size the item by
+         * the pre-pass and decode it again (rare) */
+        for (uint32_t k = 0; k < m; k++) {
+            if (dl[k] || exact[k]) continue;
+            uint32_t sz = 0;
+            int32_t e = 0;
+            if (lzf_host_decoded_size_batch(vals, &ioff[k], &len[k], &sz, &e, 1, maxrequestsize) || !sz) continue;
+            uint8_t *b = realloc(dec, total + sz);
+            if (!b) {
+                ret = LZF_GPU_ENOMEM;
+                goto done;
+            }
+            dec = b;
+            const uint64_t o = total;
+            total += sz;
+            g_mget_staged = total;
+            if (lzf_host_decompress_batch(vals, &ioff[k], &len[k], dec, &o, &sz, &dl[k], &er[k], 1)) continue;
+            ooff[k] = o;
         }
     }
     {
@@ -187,10 +260,12 @@ long gb_mget_payload(const uint8_t *keys, const uint64_t *key_off, const uint32_
             if (gb_put(&p, &space, &sz, 4) || gb_put(&p, &space, keys + key_off[i], sz)) goto done;
             if (e == GB_ENC_LZF) {                                 /* src/net.c:1306-1318 */
                 const uint32_t k = (uint32_t)pos[i];
-                if (!dl[k]) goto done;                             /* the reference asserts */
+                /* an item that does not decode goes out with size 0: the
+                 * release build (-DNDEBUG, CMakeLists.txt:20) compiles the
+                 * assert of src/net.c:1331 out */
                 e = GB_ENC_PLAIN;
                 vsize = dl[k];
-                vp = dec + ooff[k];
+                vp = dl[k] ? dec + ooff[k] : vals;
             }
             if (gb_put(&p, &space, &e, 1) || gb_put(&p, &space, &vsize, 4) || gb_put(&p, &space, vp, vsize))
                 goto done;
@@ -213,7 +288,11 @@ done:
     free(er);
     free(ioff);
     free(ooff);
+    free(exact);
     free(pos);
+    free(uo);
+    free(ul);
+    free(us);
     free(dec);
     return ret;
 }

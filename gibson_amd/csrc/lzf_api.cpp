@@ -34,6 +34,8 @@ hipError_t lzf_launch_compress_serial(const LzfBatch &b, hipStream_t s);
 hipError_t lzf_launch_decompress_serial(const LzfBatch &b, hipStream_t s);
 #endif
 
+int lzf_lds_order_check(void);      /* lzf_selfcheck.hip */
+
 namespace {
 
 enum KernelGen { GEN_TABLE = 0, GEN_LANE = 1, GEN_WINDOW = 2, GEN_SERIAL = 3, GEN_WTAB = 4 };
@@ -70,6 +72,29 @@ bool device_ok(int dev)
     }
     return checked[dev] == 1;
 }
+
+/* The table, lane and window generations need the LDS to run a wave's
+ * same-address ds_mskor_rtn_b32 in lane order (lzf_selfcheck.hip).  Checked
+ * once per device before their first launch; where it does not hold, compress
+ * batches go to window64.  LZF_GPU_FORCE_ORDER_FAIL=1 makes the check report
+ * a violation (tests of the fallback). */
+int g_order[64];                     /* 0 unchecked, 1 held, -1 violated, -2 probe failed */
+std::mutex g_order_mu;
+
+int lds_order_state(bool run)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -2;
+    std::lock_guard<std::mutex> lk(g_order_mu);
+    if (!g_order[dev] && run) {
+        const char *f = getenv("LZF_GPU_FORCE_ORDER_FAIL");
+        const int bad = (f && *f == '1') ? 1 : lzf_lds_order_check();
+        g_order[dev] = bad == 0 ? 1 : bad > 0 ? -1 : -2;
+    }
+    return g_order[dev];
+}
+
+bool lds_order_ok() { return lds_order_state(true) == 1; }
 
 int current_device_ok()
 {
@@ -165,7 +190,7 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s, ScratchUser who)
     if (who == SU_WTAB) {
         e = lzf_launch_compress_wtab(b, s, S.p, S.cap, &g_last_chunks);
     } else if (table) {
-        e = lzf_launch_compress_table(b, s, S.p, S.cap);
+        e = lzf_launch_compress_table(b, s, S.p, S.cap, &g_last_chunks);
     } else {
 #ifdef LZF_DIAG
         const char *ff = getenv("LZF_GPU_LANE_FORCE_FIX");
@@ -179,9 +204,9 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s, ScratchUser who)
                 if ((e = hipEventCreateWithFlags(&S.pev[k], hipEventDisableTiming)) != hipSuccess) return e;
         }
         e = lzf_launch_compress_lane(b, s, S.p, S.cap, (ff && *ff == '1') ? 1u : 0u, pipe ? S.aux : nullptr,
-                                     pipe ? S.pev : nullptr);
+                                     pipe ? S.pev : nullptr, &g_last_chunks);
 #else
-        e = lzf_launch_compress_lane(b, s, S.p, S.cap, 0u, nullptr, nullptr);
+        e = lzf_launch_compress_lane(b, s, S.p, S.cap, 0u, nullptr, nullptr, &g_last_chunks);
 #endif
     }
     if (e != hipSuccess) return e;
@@ -211,7 +236,9 @@ uint32_t lane_min_count(uint32_t max_len)
 
 hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
 {
-    switch (kernel_gen()) {
+    const KernelGen g = kernel_gen();
+    if (g != GEN_WINDOW && g != GEN_SERIAL && !lds_order_ok()) return lzf_launch_compress(b, s);
+    switch (g) {
 #ifdef LZF_DIAG
     case GEN_SERIAL: return lzf_launch_compress_serial(b, s);
 #endif
@@ -646,6 +673,43 @@ int host_batch_rc(bool compress, const uint8_t *in, const uint64_t *in_off, cons
     }
 }
 
+/* decoded sizes of host streams (the pre-pass of lzf_dsize.hip) */
+int host_dsize(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, uint32_t *out_size,
+               int32_t *err, uint32_t count, uint32_t limit)
+{
+    if (!count || !in || !in_off || !in_len || !out_size || !err) return LZF_GPU_EARG;
+    try {
+        Ctx &c = ctx();
+        DeviceGuard g(c.dev);
+        uint64_t in_end = 0;
+        for (uint32_t i = 0; i < count; i++) {
+            const uint64_t ie = in_off[i] + (in_len[i] ? in_len[i] : 1u);   /* a 0-length stream reads 1 byte */
+            if (ie > in_end) in_end = ie;
+        }
+        const size_t mb = (size_t)count * (sizeof(uint64_t) + 3 * sizeof(uint32_t));
+        uint8_t *h_in = (uint8_t *)c.h_in.get(in_end), *h_meta = (uint8_t *)c.h_meta.get(mb);
+        uint8_t *d_in = (uint8_t *)c.d_in.get(in_end), *d_meta = (uint8_t *)c.d_meta.get(mb);
+        memcpy(h_in, in, in_end);
+        memcpy(h_meta, in_off, count * sizeof(uint64_t));
+        memcpy(h_meta + count * sizeof(uint64_t), in_len, count * sizeof(uint32_t));
+        const size_t res = count * (sizeof(uint64_t) + sizeof(uint32_t));
+        check(hipMemcpyAsync(d_in, h_in, in_end, hipMemcpyHostToDevice, c.stream), "hipMemcpyAsync");
+        check(hipMemcpyAsync(d_meta, h_meta, res, hipMemcpyHostToDevice, c.stream), "hipMemcpyAsync");
+        check(lzf_launch_dsize(d_in, (const uint64_t *)d_meta, (const uint32_t *)(d_meta + count * sizeof(uint64_t)),
+                               (uint32_t *)(d_meta + res), (int32_t *)(d_meta + res + count * sizeof(uint32_t)), count,
+                               limit, c.stream),
+              "kernel launch");
+        check(hipMemcpyAsync(h_meta + res, d_meta + res, mb - res, hipMemcpyDeviceToHost, c.stream),
+              "hipMemcpyAsync");
+        check(hipStreamSynchronize(c.stream), "hipStreamSynchronize");
+        memcpy(out_size, h_meta + res, count * sizeof(uint32_t));
+        memcpy(err, h_meta + res + count * sizeof(uint32_t), count * sizeof(int32_t));
+        return LZF_GPU_OK;
+    } catch (const LzfFail &f) {
+        return f.code;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -693,11 +757,14 @@ int lzf_gpu_compress_batch(const uint8_t *in, const uint64_t *in_off, const uint
                            uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
                            uint32_t *out_len, uint32_t count, uint32_t max_in_len, void *stream)
 {
-    if (!count || !in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len || !max_in_len)
-        return LZF_GPU_EARG;
+    if (!count || !in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len) return LZF_GPU_EARG;
     if (max_in_len > LZF_GPU_MAX_VALUE) return LZF_GPU_EARG;
     int rc = current_device_ok();
     if (rc) return rc;
+    if (!max_in_len)                  /* every value empty: out_len 0 each (src/lzf_c.c:131) */
+        return hipMemsetAsync(out_len, 0, (size_t)count * sizeof(uint32_t), (hipStream_t)stream) == hipSuccess
+                   ? LZF_GPU_OK
+                   : LZF_GPU_ELAUNCH;
     LzfBatch b{in, in_off, in_len, out, out_off, out_cap, out_len, nullptr, count, max_in_len};
     const hipError_t e = launch_compress(b, (hipStream_t)stream);
     return e == hipSuccess ? LZF_GPU_OK : code_of(e);
@@ -755,6 +822,23 @@ int lzf_host_decompress_batch(const uint8_t *in, const uint64_t *in_off, const u
     return host_batch_rc(false, in, in_off, in_len, out, out_off, out_cap, out_len, err, count);
 }
 
+int lzf_gpu_decoded_size_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                               uint32_t *out_size, int32_t *err, uint32_t count, uint32_t out_limit, void *stream)
+{
+    if (!count || !in || !in_off || !in_len || !out_size || !err) return LZF_GPU_EARG;
+    int rc = current_device_ok();
+    if (rc) return rc;
+    return lzf_launch_dsize(in, in_off, in_len, out_size, err, count, out_limit, (hipStream_t)stream) == hipSuccess
+               ? LZF_GPU_OK
+               : LZF_GPU_ELAUNCH;
+}
+
+int lzf_host_decoded_size_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                                uint32_t *out_size, int32_t *err, uint32_t count, uint32_t out_limit)
+{
+    return host_dsize(in, in_off, in_len, out_size, err, count, out_limit);
+}
+
 uint64_t lzf_gpu_kv_frame_work_size(uint32_t count)
 {
     return lzf_frame_work_bytes(count);
@@ -786,6 +870,21 @@ int lzf_gpu_kv_frame(const uint8_t *keys, const uint64_t *key_off, const uint32_
                                                                                     : LZF_GPU_ELAUNCH;
 }
 
+int lzf_gpu_selfcheck(void)
+{
+    int rc = current_device_ok();
+    if (rc) return rc;
+    const int st = lds_order_state(true);
+    return st == 1 ? 1 : st == -1 ? 0 : LZF_GPU_ELAUNCH;
+}
+
+int lzf_gpu_lds_order_probe(void)
+{
+    int rc = current_device_ok();
+    if (rc) return rc;
+    return lzf_lds_order_check();
+}
+
 const char *lzf_gpu_kernel_info(void)
 {
     static thread_local std::string s;
@@ -799,7 +898,7 @@ const char *lzf_gpu_kernel_info(void)
         break;
     case GEN_WTAB:
         s = std::string("compress=wtab(cand_q1+wparse; window64 past 64 KiB) decompress=") +
-            lzf_decompress_kernel_name() + " scratch_chunks=" + std::to_string(g_last_chunks);
+            lzf_decompress_kernel_name();
         break;
     case GEN_LANE:
         s = std::string("compress=lane(cand+parse; window64 past 64 KiB or below ") +
@@ -817,6 +916,12 @@ const char *lzf_gpu_kernel_info(void)
             std::to_string(lane_min_count(65536u)) + " of <= 64 KiB) decompress=" +
             (lane_decoder() ? "lane" : lzf_decompress_kernel_name());
         break;
+    }
+    {
+        const int st = lds_order_state(false);
+        s += std::string(" lds_order=") + (st == 1 ? "held" : st == -1 ? "violated(compress->window64)"
+                                           : st == -2 ? "probe-failed(compress->window64)" : "unchecked");
+        if (g_last_chunks) s += " scratch_chunks=" + std::to_string(g_last_chunks);
     }
     return s.c_str();
 }

@@ -880,7 +880,8 @@ size_t lzf_table_scratch_per_value(uint32_t max_len)
 
 bool lzf_table_compress_supported(uint32_t max_len) { return max_len <= LZF_SLOTS; }
 
-hipError_t lzf_launch_compress_table(const LzfBatch &b, hipStream_t s, void *scratch, size_t scratch_bytes)
+hipError_t lzf_launch_compress_table(const LzfBatch &b, hipStream_t s, void *scratch, size_t scratch_bytes,
+                                     uint32_t *chunks)
 {
     if (b.max_len > LZF_SLOTS) return hipErrorInvalidValue;
     const uint64_t rstride = rec_stride(b.max_len), bstride = rec_bstride(b.max_len);
@@ -903,6 +904,7 @@ hipError_t lzf_launch_compress_table(const LzfBatch &b, hipStream_t s, void *scr
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         cus = 256;
     hipError_t e;
+    if (chunks) *chunks = (uint32_t)((b.count + chunk - 1u) / chunk);
     for (uint64_t first = 0; first < b.count; first += chunk) {
         const uint32_t cnt = (uint32_t)((b.count - first) < chunk ? (b.count - first) : chunk);
         LzfBatch c = b;

@@ -73,7 +73,8 @@ struct LzfRecScratch {
 };
 
 /* launchers, defined next to their kernels; return hipSuccess or the error */
-hipError_t lzf_launch_compress_table(const LzfBatch &b, hipStream_t s, void *scratch, size_t scratch_bytes);
+hipError_t lzf_launch_compress_table(const LzfBatch &b, hipStream_t s, void *scratch, size_t scratch_bytes,
+                                     uint32_t *chunks);
 size_t lzf_table_scratch_per_value(uint32_t max_len);
 bool lzf_table_compress_supported(uint32_t max_len);
 hipError_t lzf_launch_compress_wtab(const LzfBatch &b, hipStream_t s, void *scratch, size_t scratch_bytes,
@@ -81,11 +82,13 @@ hipError_t lzf_launch_compress_wtab(const LzfBatch &b, hipStream_t s, void *scra
 size_t lzf_wtab_scratch_per_value(uint32_t max_len);
 bool lzf_wtab_compress_supported(uint32_t max_len);
 hipError_t lzf_launch_decompress_lane(const LzfBatch &b, hipStream_t s);
+hipError_t lzf_launch_dsize(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, uint32_t *out_size,
+                            int32_t *err, uint32_t count, uint32_t limit, hipStream_t s);
 /* aux / ev (4 events) optional: chunks pipelined over s (kernel 1) and aux
  * (kernel 2); s is joined with aux before returning */
 hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scratch,
                                     size_t scratch_bytes, uint32_t force_fix, hipStream_t aux,
-                                    hipEvent_t *ev);
+                                    hipEvent_t *ev, uint32_t *chunks);
 size_t lzf_lane_scratch_per_value(uint32_t max_len);
 bool lzf_lane_compress_supported(uint32_t max_len);
 hipError_t lzf_launch_compress(const LzfBatch &b, hipStream_t s);

@@ -511,7 +511,10 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                      * an earlier same-slot position of this window) */
                     const uint32_t lprev = same && ppos < w0 ? (uint32_t)E[ppos] : 0u;
                     uint32_t le = !same ? (0x10000u | prev) : ppos >= w0 ? (ppos - w0) : (0x10000u | lprev);
-                    while (__ballot(!(le & 0x10000u)))
+                    /* six doublings resolve any chain inside 64 lanes; the cap bounds
+                     * the loop even if the lane order failed (then lzf_selfcheck.hip
+                     * has already routed compress batches away from this kernel) */
+                    for (uint32_t r_ = 0; r_ < 6u && __ballot(!(le & 0x10000u)); r_++)
                         le = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((le & 0x10000u) ? lane : le) << 2), (int)le);
                     if (act[j]) E[p[j]] = (uint16_t)le;
                     ln_wave_fence();
@@ -531,7 +534,9 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
 #pragma unroll
                     for (uint32_t j = 0; j < WIN; j++) {
                         if (cur[j]) {
-                            const uint32_t e = E[(cur[j] >> IDB) - 1u];
+                            /* links go to earlier positions; anything else ends the walk */
+                            const uint32_t e0 = E[(cur[j] >> IDB) - 1u];
+                            const uint32_t e = (e0 >> IDB) < (cur[j] >> IDB) ? e0 : 0u;
                             cur[j] = e;
                             if (e && (e & IDM) == (m[j] & IDM)) { q1[j] = e >> IDB; cur[j] = 0u; }
                             need |= cur[j] != 0u;
@@ -1582,7 +1587,7 @@ bool lzf_lane_compress_supported(uint32_t max_len)
 
 hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scratch,
                                     size_t scratch_bytes, uint32_t force_fix, hipStream_t aux,
-                                    hipEvent_t *ev)
+                                    hipEvent_t *ev, uint32_t *chunks)
 {
     if (!lzf_lane_compress_supported(b.max_len)) return hipErrorInvalidValue;
     const uint64_t cstride = lane_cstride(b.max_len), bstride = lane_bstride(b.max_len);
@@ -1599,6 +1604,7 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
         const uint64_t quarter = (b.count + 3u) / 4u;
         if (quarter < chunk) chunk = quarter < 1024u ? (b.count < 1024u ? b.count : 1024u) : quarter;
     }
+    if (chunks) *chunks = (uint32_t)((b.count + chunk - 1u) / chunk);
     LzfLaneScratch sc[2];
     for (int h = 0; h < 2; h++) {
         uint8_t *base = (uint8_t *)scratch + (pipe ? h * half : 0);

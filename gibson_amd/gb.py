@@ -44,6 +44,8 @@ def _L():
     L.gb_lentab_del.argtypes = [vp, u64]
     L.gb_lentab_size.restype = ctypes.c_size_t
     L.gb_lentab_size.argtypes = [vp]
+    L.gb_mget_last_staged.restype = u64
+    L.gb_mget_last_staged.argtypes = []
     _BOUND.add(id(L))
     return L
 
@@ -112,6 +114,11 @@ def mget_payload(items, elements, maxrequestsize, max_response, orig_lens=None, 
                              1 if reply_header else 0, _p(out))
     _check(r, "gb_mget_payload")
     return bytes(out[:r]) if r > 0 else None
+
+
+def mget_last_staged():
+    """Bytes of decode arena the last mget_payload of this thread staged."""
+    return int(_L().gb_mget_last_staged())
 
 
 class LenTab:

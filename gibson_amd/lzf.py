@@ -106,6 +106,14 @@ def _load(path):
     L.lzf_gpu_release.argtypes = []
     L.lzf_gpu_kernel_info.restype = ctypes.c_char_p
     L.lzf_gpu_kernel_info.argtypes = []
+    L.lzf_gpu_selfcheck.restype = ctypes.c_int
+    L.lzf_gpu_selfcheck.argtypes = []
+    L.lzf_gpu_lds_order_probe.restype = ctypes.c_int
+    L.lzf_gpu_lds_order_probe.argtypes = []
+    L.lzf_gpu_decoded_size_batch.restype = ctypes.c_int
+    L.lzf_gpu_decoded_size_batch.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp]
+    L.lzf_host_decoded_size_batch.restype = ctypes.c_int
+    L.lzf_host_decoded_size_batch.argtypes = [vp, vp, vp, vp, vp, u32, u32]
     L.lzf_gpu_kv_frame_work_size.restype = u64
     L.lzf_gpu_kv_frame_work_size.argtypes = [u32]
     L.lzf_gpu_kv_frame.restype = ctypes.c_int
@@ -114,6 +122,24 @@ def _load(path):
     del i32
     _LOADED[path] = L
     return L
+
+
+def selfcheck():
+    """lzf_gpu_selfcheck(): 1 when the lane-ordered LDS exchange held on the
+    current device, 0 when compress batches fall back to window64."""
+    return int(lib().lzf_gpu_selfcheck())
+
+
+def lds_order_probe():
+    """lzf_gpu_lds_order_probe(): mismatching lanes of a fresh probe run."""
+    return int(lib().lzf_gpu_lds_order_probe())
+
+
+def decoded_size_batch(inp, in_off, in_len, out_size, err, out_limit, stream=None):
+    """Device pre-pass: out_size/err of lzf_decompress at out_len = out_limit."""
+    _check(lib().lzf_gpu_decoded_size_batch(_ptr(inp), _ptr(in_off), _ptr(in_len), _ptr(out_size), _ptr(err),
+                                            int(in_off.numel()), int(out_limit), _stream_handle(stream)),
+           "lzf_gpu_decoded_size_batch")
 
 
 def kernel_info():

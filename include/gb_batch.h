@@ -92,17 +92,25 @@ int gb_mset(const uint8_t *v, uint32_t vlen, uint32_t nkeys, uint32_t compressio
  * gbClientEnqueueData (src/net.c:1162-1205) in front.  Item i: key
  * keys + key_off[i] (key_len[i] bytes), stored bytes vals + val_off[i]
  * (val_size[i] bytes; for an LZF item the stream), enc[i]; orig_len (may be
- * NULL) gives an LZF item's decoded length (0 = unknown: decoded with
- * out_len = maxrequestsize, as src/net.c:1309-1315).  out holds
+ * NULL) gives an LZF item's decoded length (0 = unknown: sized by the
+ * device pre-pass at out_len = maxrequestsize, as src/net.c:1309-1315, then
+ * decoded into a slot of that size).  out holds
  * (reply_header ? 7 : 0) + max_response bytes.
- * Returns the frame length, 0 when the payload exceeds max_response (the
- * reference's CHECK_SPACE, src/net.c:1272-1277) or an LZF item does not
- * decode (the reference asserts, src/net.c:1237), or a negative error.
+ * An LZF item that does not decode at maxrequestsize goes out as PLAIN with
+ * size 0, as the release build does (its assert, src/net.c:1331, is compiled
+ * out by -DNDEBUG, CMakeLists.txt:20).  Returns the frame length, 0 when the
+ * payload exceeds max_response (the reference's CHECK_SPACE,
+ * src/net.c:1272-1277), or a negative error.
  */
 long gb_mget_payload(const uint8_t *keys, const uint64_t *key_off, const uint32_t *key_len,
                      const uint8_t *vals, const uint64_t *val_off, const uint32_t *val_size,
                      const uint8_t *enc, const uint32_t *orig_len, uint32_t count, uint32_t elements,
                      uint32_t maxrequestsize, uint64_t max_response, int reply_header, uint8_t *out);
+/* bytes of decode arena the calling thread's last gb_mget_payload staged:
+ * the LZF items' decoded sizes (side table, capped at maxrequestsize, or the
+ * device pre-pass lzf_host_decoded_size_batch), never maxrequestsize per
+ * item; 0 when the payload was known to exceed max_response up front */
+uint64_t gb_mget_last_staged(void);
 
 /* the original-length side table (open addressing, grows; not thread-safe,
  * like the reference's single-threaded store) */

@@ -48,7 +48,8 @@ extern "C" {
  * out_len[i] (0 = does not fit, exactly when src/lzf_c.c returns 0; the
  * bytes at out then are unspecified, and nothing is ever written at or past
  * out_cap[i]).  max_in_len is an upper bound on every in_len[i] (selects the
- * kernel's LDS plan without reading device memory).
+ * kernel's LDS plan without reading device memory); max_in_len 0 declares an
+ * all-empty batch (every out_len 0, src/lzf_c.c:131).
  * The server policy of src/query.c:385 is out_cap[i] = in_len[i] - 4.
  */
 int lzf_gpu_compress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
@@ -68,6 +69,22 @@ int lzf_gpu_decompress_batch(const uint8_t *in, const uint64_t *in_off, const ui
                              uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
                              uint32_t *out_len, int32_t *err, uint32_t count,
                              uint32_t max_out_cap, void *stream);
+
+/*
+ * Decoded-size pre-pass: out_size[i] gets the length lzf_decompress would
+ * return for stream i with out_len = out_limit (0 on failure) and err[i]
+ * its errno (0, E2BIG or EINVAL in the reference's check order,
+ * src/lzf_d.c:64-146); nothing is decoded.  For MGET items without an
+ * original-length side-table entry: size them at out_limit = maxrequestsize
+ * (src/net.c:1309-1315), then decode into exact slots (gb_mget_payload, or
+ * val_len for lzf_gpu_kv_frame).  As for decompress, in[in_off[i]] must be
+ * readable even when in_len[i] is 0.
+ */
+int lzf_gpu_decoded_size_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                               uint32_t *out_size, int32_t *err, uint32_t count, uint32_t out_limit,
+                               void *stream);
+int lzf_host_decoded_size_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                                uint32_t *out_size, int32_t *err, uint32_t count, uint32_t out_limit);
 
 /*
  * Fill `count` values of n bytes each, value k at out[k*n], with synthetic
@@ -131,6 +148,18 @@ int lzf_gpu_kv_frame(const uint8_t *keys, const uint64_t *key_off, const uint32_
  * staging buffers; later calls allocate them again.  Each thread's staging
  * buffers are also freed when the thread exits. */
 void lzf_gpu_release(void);
+
+/* One-time self-check of the current device (run lazily before the first
+ * compress launch, or here): the table / lane / window compressor kernels
+ * need the LDS to execute a wave's same-address ds_mskor_rtn_b32 in lane
+ * order (gibson_amd/csrc/lzf_selfcheck.hip).  Returns 1 when that held (the
+ * measured routing is used), 0 when it did not (compress batches then run
+ * window64, which needs no ordering), or a negative LZF_GPU_E* code.  The
+ * result also appears in lzf_gpu_kernel_info() as lds_order=... */
+int lzf_gpu_selfcheck(void);
+/* The probe itself, run again: mismatching lanes over 16 collision patterns
+ * of 1024 waves (0 = lane order held), or a negative LZF_GPU_E* code. */
+int lzf_gpu_lds_order_probe(void);
 
 /* Which kernel generation the batch calls dispatch to (diagnostics):
  * returns a static string such as "compress=window64 decompress=tokpar". */

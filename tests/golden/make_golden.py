@@ -162,6 +162,11 @@ DIGEST_CONFIGS = [
     (2, 2, 0x5EED0003, 65536, 262144),
     (3, 0, 0x5EED0004, 8192, 65536),
     (4, 3, 0x5EED0005, 16384, 65536),
+    # the production routes at their real batch sizes: >= 163 840 values of
+    # <= 4 KiB take the lane small class, >= 81 920 of <= 16 KiB the table
+    # generation (lzf_api.cpp lane_min_count)
+    (1, 1, 0x5EED0002, 4096, 262144),
+    (4, 3, 0x5EED0005, 16384, 131072),
 ]
 
 

@@ -121,3 +121,50 @@ def test_mget_payload_matches_reference_frame(oracle, side_table):
             exp = oracle.kv_frame(items, len(items), maxresp, 4 << 20, reply_header=hdr)
             got = mget_payload(items, len(items), 4 << 20, maxresp, orig_lens=lens, reply_header=hdr)
             assert got == exp
+
+
+@pytest.mark.gpu
+def test_mget_unknown_lengths_staged_exact(oracle):
+    # 1000 LZF items with no side-table entry: the device pre-pass sizes
+    # them, so the decode arena is their decoded bytes, not 1000 x 4 MiB
+    # (the reference decodes each at out_len = maxrequestsize, src/net.c:1309)
+    from gibson_amd.gb import mget_last_staged, mget_payload
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rnd = random.Random(21)
+    items, decoded = [], 0
+    for i in range(1000):
+        v = synth(rnd.randrange(4), 0x5EED0A20, i, rnd.choice([300, 4096, 20000]))
+        s = oracle.compress(v, len(v) + len(v) // 16 + 64)
+        assert s
+        items.append((b"k%d" % i, 1, s))
+        decoded += len(v)
+    exp = oracle.kv_frame(items, len(items), 1 << 30, 4 << 20)
+    got = mget_payload(items, len(items), 4 << 20, 1 << 30, orig_lens=[0] * len(items))
+    assert got == exp
+    staged = mget_last_staged()
+    assert decoded <= staged < 2 * decoded, (staged, decoded)
+    # a payload known to exceed max_response stages nothing
+    assert mget_payload(items, len(items), 4 << 20, 100000) is None
+    assert mget_last_staged() == 0
+
+
+@pytest.mark.gpu
+def test_mget_stale_and_oversize_side_table(oracle):
+    # side-table lengths that are too small (stale) are re-sized by the
+    # pre-pass; an item longer than maxrequestsize does not decode and goes
+    # out with size 0, as the release build of src/net.c:1306-1335 does
+    from gibson_amd.gb import mget_payload
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rnd = random.Random(22)
+    items, lens = [], []
+    for i in range(60):
+        v = synth(rnd.randrange(4), 0x5EED0A21, i, rnd.choice([500, 3000, 9000]))
+        s = oracle.compress(v, len(v) + len(v) // 16 + 64)
+        items.append((b"key%d" % i, 1, s))
+        lens.append(rnd.choice([len(v), max(1, len(v) // 2), len(v) + 7, 0]))
+    for maxreq in (4 << 20, 4096):
+        exp = oracle.kv_frame(items, len(items), 1 << 30, maxreq)
+        got = mget_payload(items, len(items), maxreq, 1 << 30, orig_lens=lens)
+        assert got == exp, maxreq

@@ -142,6 +142,65 @@ def test_batch_decompress_golden(golden, oracle):
     assert not bad, f"{len(bad)} mismatches, first: {bad[:5]}"
 
 
+def test_decoded_size_prepass_golden(golden, oracle):
+    # the pre-pass (lzf_dsize.hip) against the reference's decode length and
+    # errno on the whole golden decoder corpus: valid, tight, truncated at
+    # every cut, corrupted and random streams
+    import gibson_amd
+    from tests.gpu_batch import _pack
+    from tests.test_oracle import decoder_cases
+    cases = list(decoder_cases(golden, oracle))
+    streams = [s for _, s in cases]
+    bad = []
+    for limit in sorted({c["out_len"] for c, _ in cases}):
+        sel = [(c, s) for c, s in cases if c["out_len"] == limit]
+        arena, offs = _pack([s for _, s in sel])
+        d_in = torch.from_numpy(arena).cuda()
+        d_off = torch.from_numpy(offs).cuda()
+        d_len = torch.tensor([len(s) for _, s in sel], dtype=torch.int32, device="cuda")
+        size = torch.full((len(sel),), -1, dtype=torch.int32, device="cuda")
+        err = torch.full((len(sel),), -1, dtype=torch.int32, device="cuda")
+        gibson_amd.decoded_size_batch(d_in, d_off, d_len, size, err, limit)
+        torch.cuda.synchronize()
+        for (c, _), z, e in zip(sel, size.cpu().tolist(), err.cpu().tolist()):
+            if z != c["result"] or e != c["errno"]:
+                bad.append((c.get("tag"), limit, c["result"], c["errno"], z, e))
+    assert streams and not bad, f"{len(bad)} mismatches, first: {bad[:5]}"
+
+
+def test_lds_lane_order_selfcheck():
+    # the probe the table / lane / window generations depend on
+    # (lzf_selfcheck.hip), run as a library entry point; and the library's
+    # one-time check is visible in kernel_info
+    import gibson_amd
+    assert gibson_amd.lds_order_probe() == 0
+    assert gibson_amd.selfcheck() == 1
+    assert "lds_order=held" in gibson_amd.kernel_info()
+
+
+def test_lds_order_violation_falls_back_to_window64(golden, tmp_path):
+    # a failed check routes compress batches to window64 (order-free): the
+    # results stay bit-exact.  The check is per process, so in a child.
+    import subprocess
+    import sys
+    code = (
+        "import os, sys; sys.path.insert(0, %r)\n"
+        "from tests.oracle_lib import synth, Oracle\n"
+        "from tests.gpu_batch import gpu_compress\n"
+        "import gibson_amd\n"
+        "vals = [synth(k %% 4, 0x5EED0A30, k, 4096 * (1 + k %% 16)) for k in range(64)]\n"
+        "caps = [len(v) - 4 for v in vals]\n"
+        "o = Oracle()\n"
+        "assert gpu_compress(vals, caps) == [o.compress(v, c) for v, c in zip(vals, caps)]\n"
+        "assert gibson_amd.selfcheck() == 0\n"
+        "info = gibson_amd.kernel_info()\n"
+        "assert 'lds_order=violated' in info, info\n"
+        "print('ok', info)\n") % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LZF_GPU_FORCE_ORDER_FAIL="1", LZF_GPU_LANE_MIN="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
 @pytest.mark.parametrize("gen", ["window", "serial", "lane-decoder"])
 def test_batch_decompress_other_generations(golden, oracle, monkeypatch, gen):
     if gen == "lane-decoder":
@@ -397,6 +456,11 @@ CONFIGS = [
     (2, 0x5EED0003, 65536, 262144),
     (0, 0x5EED0004, 8192, 65536),   # the table generation (values past 4 KiB)
     (3, 0x5EED0005, 16384, 65536),
+    # the production routes at the configs' real per-GPU counts: 262 144
+    # values of 4 KiB run the lane small class, 131 072 of 16 KiB the table
+    # generation (below 163 840 / 81 920 values both would run window64)
+    (1, 0x5EED0002, 4096, 262144),
+    (3, 0x5EED0005, 16384, 131072),
 ]
 
 
