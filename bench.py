@@ -167,15 +167,22 @@ def cpu_baseline(kind, seed, n, count, threads, decode_only=False):
 
 
 def _traffic(workload, kernel, count):
-    """HBM bytes per launch of `kernel` from the committed PMC summary
-    (profiles/traffic_<workload>.json, tools/traffic.py: 2*FETCH_SIZE +
-    WRITE_SIZE, KiB -> B, gfx950 read-side correction), or None."""
+    """(HBM bytes per launch of `kernel`, where they come from) from the
+    committed PMC summary (profiles/traffic_<workload>.json, tools/traffic.py:
+    2*FETCH_SIZE + WRITE_SIZE, KiB -> B; the x2 read correction is calibrated
+    for both the streaming and the one-line-per-lane loads, profiles/r03/
+    fetch_calib.txt), stamped with the commit the counters were taken at --
+    a per-value figure times this launch's count, not a counter of this run;
+    (None, None) when there is none."""
     f = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
     try:
         t = json.load(open(f))
-        return int(t["kernels"][kernel]["bytes_per_value"] * count)
+        return (int(t["kernels"][kernel]["bytes_per_value"] * count),
+                {"file": os.path.relpath(f, ROOT), "profile_commit": t.get("profile_commit"),
+                 "bytes_per_value": round(t["kernels"][kernel]["bytes_per_value"], 1),
+                 "read_correction": (t.get("calibration") or {}).get("read_correction", 2.0)})
     except (OSError, KeyError, ValueError):
-        return None
+        return None, None
 
 
 def _cpu_model():
@@ -359,7 +366,8 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBPS, 5),
-                "traffic": _traffic(a.workload, dom, count),
+                "traffic": _traffic(a.workload, dom, count)[0],
+                "traffic_source": _traffic(a.workload, dom, count)[1],
                 "algorithmic_bytes": kern[dom][0],
                 "per_kernel_ms": {k: round(v[1] * 1e3, 3) for k, v in kern.items()},
                 "per_kernel_GBps": {k: round(v[0] / v[1] / 1e9, 2) for k, v in kern.items()},
@@ -488,7 +496,8 @@ def main_decompress(a, world, rank, dev, cfg_idx, kind, seed, n, count):
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBPS, 5),
-                "traffic": _traffic(f"{a.workload}_decode", "lzf_decompress", count),
+                "traffic": _traffic(f"{a.workload}_decode", "lzf_decompress", count)[0],
+                "traffic_source": _traffic(f"{a.workload}_decode", "lzf_decompress", count)[1],
                 "algorithmic_bytes": dec_bytes,
                 "per_kernel_ms": {"lzf_decompress": round(t_dec * 1e3, 3)},
             },
