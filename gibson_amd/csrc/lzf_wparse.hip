@@ -57,30 +57,52 @@
 #ifndef KQ_PF
 #define KQ_PF 4u                   /* blocks of input bytes in flight per worker lane */
 #endif
-static_assert(KQ_WIN % 5u == 0u, "the exchanges go in groups of 5 windows");
+#ifndef KQ_XCHG
+/* 1: the table step by lane-ordered exchanges; 0: plain T reads and
+ * last-writer writes with the window's same-slot lanes from 16 ballots in the
+ * workers (no returning atomics: 29.5 vs 14.5 ms for 64 K x 64 KiB, kept as
+ * an option) */
+#define KQ_XCHG 1
+#endif
 
 __device__ __forceinline__ uint32_t kq_lds_addr(const void *p)
 {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
 }
 
-/* five windows' exchanges, issued in window (= position) order, then one
- * wait.  The LDS runs one wave's same-address ds_mskor_rtn_b32 in lane order
- * (tools/lds_mskor_order.hip; checked at run time by lzf_gpu_selfcheck), so
- * each lane gets the latest earlier same-slot position -- the table's or an
- * earlier lane's -- and the highest lane's position is what stays. */
+/* the block's 15 exchanges, issued in window (= position) order with one
+ * wait at the end.  The LDS runs one wave's same-address ds_mskor_rtn_b32
+ * in lane order (tools/lds_mskor_order.hip; checked at run time by
+ * lzf_selfcheck.hip), so each lane gets the latest earlier same-slot
+ * position -- the table's or an earlier lane's -- and the highest lane's
+ * position is what stays; and one wave's LDS operations execute in order,
+ * so the table is updated in position order.  Three asm groups of five: the
+ * later groups take the earlier results as in-out operands, so nothing reads
+ * a result before the single wait. */
 #define KQ_X(i_) "ds_mskor_rtn_b32 %" #i_ ", %[a" #i_ "], %[m" #i_ "], %[d" #i_ "]\n\t"
-#define KQ_IN(i_) [a##i_] "v"(a[i_]), [m##i_] "v"(m[i_]), [d##i_] "v"(d[i_])
-__device__ __forceinline__ void kq_xchg5(uint32_t (&r)[5], const uint32_t (&a)[5], const uint32_t (&m)[5],
-                                         const uint32_t (&d)[5])
+#define KQ_IN(i_, o_) [a##i_] "v"(a[(o_) + i_]), [m##i_] "v"(m[(o_) + i_]), [d##i_] "v"(d[(o_) + i_])
+__device__ __forceinline__ void kq_xchg15(uint32_t (&r)[15], const uint32_t (&a)[15], const uint32_t (&m)[15],
+                                          const uint32_t (&d)[15])
 {
-    asm volatile(KQ_X(0) KQ_X(1) KQ_X(2) KQ_X(3) KQ_X(4) "s_waitcnt lgkmcnt(0)"
+    asm volatile(KQ_X(0) KQ_X(1) KQ_X(2) KQ_X(3) KQ_X(4)
                  : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4])
-                 : KQ_IN(0), KQ_IN(1), KQ_IN(2), KQ_IN(3), KQ_IN(4)
+                 : KQ_IN(0, 0), KQ_IN(1, 0), KQ_IN(2, 0), KQ_IN(3, 0), KQ_IN(4, 0)
+                 : "memory");
+    asm volatile(KQ_X(0) KQ_X(1) KQ_X(2) KQ_X(3) KQ_X(4)
+                 : "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7]), "=&v"(r[8]), "=&v"(r[9]),
+                   "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4])
+                 : KQ_IN(0, 5), KQ_IN(1, 5), KQ_IN(2, 5), KQ_IN(3, 5), KQ_IN(4, 5)
+                 : "memory");
+    asm volatile(KQ_X(0) KQ_X(1) KQ_X(2) KQ_X(3) KQ_X(4) "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(r[10]), "=&v"(r[11]), "=&v"(r[12]), "=&v"(r[13]), "=&v"(r[14]),
+                   "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]),
+                   "+v"(r[5]), "+v"(r[6]), "+v"(r[7]), "+v"(r[8]), "+v"(r[9])
+                 : KQ_IN(0, 10), KQ_IN(1, 10), KQ_IN(2, 10), KQ_IN(3, 10), KQ_IN(4, 10)
                  : "memory");
 }
 #undef KQ_X
 #undef KQ_IN
+static_assert(KQ_WIN == 15u, "kq_xchg15 issues 15 windows");
 
 /* bytes p, p+1, p+2 (p + 3 <= n) with one 4-byte load moved back inside the
  * value near its end */
@@ -102,7 +124,14 @@ template <uint32_t V> struct KqIc { static constexpr uint32_t value = V; };
 __global__ __launch_bounds__(KQ_THREADS) void lzf_cand_q1_kernel(LzfBatch bt, uint16_t *cand, uint64_t cstride)
 {
     __shared__ __attribute__((aligned(16))) uint16_t T[LZF_SLOTS + 64u];  /* slot -> latest position, 0: none; + dummies */
+    /* S: per position, KQ_XCHG: the exchange operands [T dword address |
+     * half bit, data]; else [slot:16 | last of its slot in the window:1 |
+     * nearest earlier same-slot lane (127: none):7].  O: its q1 */
+#if KQ_XCHG
+    __shared__ uint2 S[2u * KQ_BLK];
+#else
     __shared__ uint32_t S[2u * KQ_BLK];
+#endif
     __shared__ uint16_t O[2u * KQ_BLK];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6, j = w - 1u;
     for (uint32_t v = blockIdx.x; v < bt.count; v += gridDim.x) {
@@ -123,29 +152,51 @@ __global__ __launch_bounds__(KQ_THREADS) void lzf_cand_q1_kernel(LzfBatch bt, ui
         const auto step = [&](auto ps, uint32_t t) {
             constexpr uint32_t PS = decltype(ps)::value;                  /* t % KQ_PF */
             if (w == 0u) {
+#ifdef KQ_ABL_B     /* diagnostics: no table-wave work */
+                if (false) {
+#else
                 if (t >= 1u && t <= nb) {                                  /* B(t-1) */
-                    const uint32_t k = t - 1u, B = KQ_BLK * k;
-                    const uint32_t *Sk = S + KQ_BLK * (k & 1u);
+#endif
+                    const uint32_t k = t - 1u;
                     uint16_t *Ok = O + KQ_BLK * (k & 1u);
-                    const uint32_t tb = kq_lds_addr(T);
+#if KQ_XCHG
+                    const uint2 *Sk = S + KQ_BLK * (k & 1u);
+                    uint32_t xa[15], xm[15], xd[15], xr[15];
+                    uint2 e[15];
 #pragma unroll
-                    for (uint32_t g = 0; g < KQ_WIN; g += 5u) {
-                        uint32_t xa[5], xm[5], xd[5], xr[5], xs[5];
+                    for (uint32_t i = 0; i < 15u; i++) e[i] = Sk[64u * i + lane];
 #pragma unroll
-                        for (uint32_t u = 0; u < 5u; u++) {
-                            const uint32_t i = g + u;
-                            const uint32_t e = Sk[64u * i + lane];
-                            /* a position past the value exchanges in its lane's own dummy */
-                            const uint32_t h = (e >> 16) ? (e & 0xFFFFu) : LZF_SLOTS + lane;
-                            xs[u] = (h & 1u) << 4;
-                            xa[u] = tb + 4u * (h >> 1);
-                            xm[u] = 0xFFFFu << xs[u];
-                            xd[u] = ((B + 64u * i + lane) & 0xFFFFu) << xs[u];
-                        }
-                        kq_xchg5(xr, xa, xm, xd);
-#pragma unroll
-                        for (uint32_t u = 0; u < 5u; u++) Ok[64u * (g + u) + lane] = (uint16_t)(xr[u] >> xs[u]);
+                    for (uint32_t i = 0; i < 15u; i++) {
+                        xa[i] = e[i].x & ~1u;
+                        xm[i] = (e[i].x & 1u) ? 0xFFFF0000u : 0x0000FFFFu;
+                        xd[i] = e[i].y;
                     }
+                    kq_xchg15(xr, xa, xm, xd);
+#pragma unroll
+                    for (uint32_t i = 0; i < 15u; i++)
+                        Ok[64u * i + lane] = (uint16_t)(xr[i] >> ((e[i].x & 1u) << 4));
+#else
+                    /* window by window: read T at the slot, then the window's
+                     * last lane of each slot writes its position (the others
+                     * write their lane's dummy, so no two lanes share an
+                     * address); a lane with an earlier same-slot lane in its
+                     * window takes that lane's position instead of T's */
+                    const uint32_t B = KQ_BLK * k, *Sk = S + KQ_BLK * (k & 1u);
+                    uint32_t e[15], r[15];
+#pragma unroll
+                    for (uint32_t i = 0; i < 15u; i++) e[i] = Sk[64u * i + lane];
+#pragma unroll
+                    for (uint32_t i = 0; i < 15u; i++) {
+                        r[i] = T[e[i] & 0xFFFFu];
+                        T[(e[i] & 0x10000u) ? (e[i] & 0xFFFFu) : LZF_SLOTS + lane] =
+                            (uint16_t)(B + 64u * i + lane);
+                    }
+#pragma unroll
+                    for (uint32_t i = 0; i < 15u; i++) {
+                        const uint32_t pl = (e[i] >> 17) & 127u;
+                        Ok[64u * i + lane] = (uint16_t)(pl < 64u ? B + 64u * i + pl : r[i]);
+                    }
+#endif
                 }
             } else {
                 if (t >= 2u && t - 2u < nb) {                              /* C(t-2) */
@@ -158,12 +209,39 @@ __global__ __launch_bounds__(KQ_THREADS) void lzf_cand_q1_kernel(LzfBatch bt, ui
                 }
                 if (t < nb) {                                              /* A(t) */
                     const uint32_t p = KQ_BLK * t + 64u * j + lane;
-                    S[KQ_BLK * (t & 1u) + 64u * j + lane] = p < np ? (dv_slot(pf[PS]) | 0x10000u) : 0u;
+                    const bool act = p < np;
+#if KQ_XCHG
+                    /* a position past the value exchanges in its lane's own dummy */
+                    const uint32_t h = act ? dv_slot(pf[PS]) : LZF_SLOTS + lane;
+                    S[KQ_BLK * (t & 1u) + 64u * j + lane] =
+                        make_uint2((kq_lds_addr(T) + 4u * (h >> 1)) | (h & 1u), (p & 0xFFFFu) << ((h & 1u) << 4));
+#else
+                    /* the window's same-slot lanes from 16 ballots of the slot
+                     * bits: the nearest earlier one (or none), and whether
+                     * this lane is its slot's last in the window */
+                    const uint32_t sl = act ? dv_slot(pf[PS]) : 0u;
+                    uint64_t eq = __ballot(act);
+#pragma unroll
+                    for (uint32_t b = 0; b < 16u; b++) {
+                        const uint64_t mb = __ballot((sl >> b) & 1u);
+                        eq &= ((sl >> b) & 1u) ? mb : ~mb;
+                    }
+                    const uint64_t lo = eq & ((1ull << lane) - 1ull), hi = eq & ~((2ull << lane) - 1ull);
+                    const uint32_t pl = lo ? 63u - (uint32_t)__builtin_clzll(lo) : 127u;
+                    S[KQ_BLK * (t & 1u) + 64u * j + lane] =
+                        act ? (sl | (hi ? 0u : 0x10000u) | (pl << 17)) : (127u << 17);
+#endif
                 }
                 const uint32_t lp = KQ_BLK * (t + KQ_PF) + 64u * j + lane;
+#ifdef KQ_ABL_L     /* diagnostics: no input loads */
+                pf[PS] = lp * 2654435761u;
+#else
                 pf[PS] = lp < np ? kq_tri(src, n, lp) : 0u;
+#endif
             }
+#ifndef KQ_ABL_S    /* diagnostics: no barrier */
             __syncthreads();
+#endif
         };
         for (uint32_t t = 0; t < nb + 2u; t += KQ_PF) {
             step(KqIc<0>{}, t);
