@@ -486,8 +486,6 @@ def main_decompress(a, world, rank, dev, cfg_idx, kind, seed, n, count):
                 "ratio": round(c_bytes_all / max(1.0, out_bytes_all), 4),
                 "kernels": gibson_amd.kernel_info(),
                 "roundtrip_ok": bad_ranks == 0,
-                "chunks": nch,
-                "chunk_values": chunk,
             },
             "roofline": {
                 "bound": "hbm",
