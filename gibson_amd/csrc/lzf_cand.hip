@@ -680,9 +680,13 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
 #endif
                 }
                 if ((word >> (q & 31u)) & 1u) {                              /* q is the ref */
-                    if (rel == 9u)
-                        rel = (src[q] == src[p] && src[q + 1u] == src[p + 1u] && src[q + 2u] == src[p + 2u]) ? 8u
-                                                                                                            : RC_DIFF;
+                    if (rel == 9u) {
+                        /* bytes q..q+2 against p..p+2 with one 4-byte load per side
+                         * (q + 3 <= p + 2 < n and p >= 1: both inside the value),
+                         * one memory wait instead of up to three */
+                        const uint32_t x_ = dv_ld4(src + q) ^ (dv_ld4(src + p - 1u) >> 8);
+                        rel = (x_ & 0xFFFFFFu) == 0u ? 8u : RC_DIFF;
+                    }
                     mode = K3_DECIDE;
                 } else if (reln) {                                           /* the record's second link */
                     q = qn;

@@ -1104,8 +1104,12 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                 }
                 if ((word >> (q & 31u)) & 1u) {                              /* q is the ref */
                     if (rel == 9u) K2_SITE(5);
-                    if (rel == 9u)
-                        rel = (src[q] == src[p] && src[q + 1u] == src[p + 1u] && src[q + 2u] == src[p + 2u]) ? 8u : 1u;
+                    if (rel == 9u) {
+                        /* one 4-byte load per side (q + 3 <= p + 2 < n, p >= 1):
+                         * one memory wait instead of up to three */
+                        const uint32_t x_ = ln_ld4(src + q) ^ (ln_ld4(src + p - 1u) >> 8);
+                        rel = (x_ & 0xFFFFFFu) == 0u ? 8u : 1u;
+                    }
                     mode = K2_DECIDE;
                 } else {
                     K2_SITE(4);
