@@ -58,6 +58,15 @@
 #ifndef CD_WALK
 #define CD_WALK    0
 #endif
+/* step 4: 1 = groups inside one long token copy without the owner search.
+ * Measured slower on every shape (same-process A/B, 5 rounds: sentence text
+ * 128 K x 64 KiB 16.02 -> 17.83 ms, Zipf 1 M x 8 KiB 20.05 -> 21.05, json
+ * 1 M x 4 KiB 7.47 -> 7.91, mixed 256 K x 16 KiB 11.48 -> 11.89): the per-round
+ * check and the per-group readlanes sit on the consumer's critical path and
+ * cost more than the owner search they skip.  Off. */
+#ifndef CD_WHOLE
+#define CD_WHOLE   0
+#endif
 /* decoder form: 1 = pipe (producer + consumer wave per stream), 0 = tokpar64 */
 #ifndef CD_PIPE
 #define CD_PIPE    1
@@ -319,8 +328,36 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
 #ifdef LZF_CD_ABLATE_OUTPUT           /* diagnostic builds only: time discovery alone */
     total = 0u;
 #endif
+#if CD_WHOLE
+    /* whole-token groups: a group that lies inside one token whose bytes all
+     * come from before the group (a literal, or a back-reference reaching 64
+     * or more back) needs no owner search and no doubling -- every lane copies
+     * its byte from the source address the token gives.  Checked per group
+     * only when the round has such a token of >= 64 bytes. */
+    const uint64_t TK = __ballot(tok);
+    const uint32_t ntok = (uint32_t)__builtin_popcountll(TK);
+    const uint32_t onext = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane + 1u) << 2), (int)Ot);
+    const uint32_t tlen = (lane + 1u < ntok ? onext : O + total) - Ot;
+    const bool whole_any = __ballot(tok && tlen >= CD_LANES && ((int32_t)tinfo < 0 || tinfo >= CD_LANES)) != 0ull;
+#endif
     for (uint32_t g = 0; g < total; g += CD_LANES) {
         const uint32_t gb = O + g;                     /* group's first output offset */
+#if CD_WHOLE
+        if (whole_any && tbase > 0u && g + CD_LANES <= total) {
+            /* the next token to start, relative to O (total: none left) */
+            const uint32_t ns = tbase < ntok ? cd_rl(Ot, tbase) - O : total;
+            const uint32_t ti = cd_rl(tinfo, tbase - 1u);
+            if (ns >= g + CD_LANES && ((int32_t)ti < 0 || ti >= CD_LANES)) {
+                const uint32_t o = gb + lane;
+                const uint32_t a = (int32_t)ti < 0 ? ((o + ti) & imask) : outr_off + ((o - ti) & omask);
+                const uint32_t b = lds[a];
+                lds[outr_off + (o & omask)] = (uint8_t)b;
+                dst[o] = (uint8_t)b;
+                cd_fence();
+                continue;
+            }
+        }
+#endif
         if (tok && Ot - gb < CD_LANES) mark[Ot - gb] = gb + 1u;
         cd_fence();
         const uint64_t S = __ballot(mark[lane] == gb + 1u);
