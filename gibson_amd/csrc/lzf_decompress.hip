@@ -67,6 +67,16 @@
 #ifndef CD_WHOLE
 #define CD_WHOLE   0
 #endif
+/* step 4: 1 = the next group's owner search issued while the current group's
+ * bytes are read (two serial LDS round trips per group instead of three).
+ * Slower (same-process A/B, 5 rounds: sentence text 128 K x 64 KiB 15.84 ->
+ * 16.19 ms, Zipf 1 M x 8 KiB 19.85 -> 20.13, json 7.46 -> 7.60, mixed 11.45 ->
+ * 11.67): with 8 waves per SIMD the consumer is bound by instruction issue,
+ * not by its LDS round trips.  Off. */
+#ifndef CD_PIPEG
+#define CD_PIPEG   0
+#endif
+static_assert(!(CD_WHOLE && CD_PIPEG), "the whole-token path keeps tbase per group");
 /* decoder form: 1 = pipe (producer + consumer wave per stream), 0 = tokpar64 */
 #ifndef CD_PIPE
 #define CD_PIPE    1
@@ -340,6 +350,23 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
     const uint32_t tlen = (lane + 1u < ntok ? onext : O + total) - Ot;
     const bool whole_any = __ballot(tok && tlen >= CD_LANES && ((int32_t)tinfo < 0 || tinfo >= CD_LANES)) != 0ull;
 #endif
+    /* the owner info of every byte of group g: marks of the token starts in
+     * the group (tagged gb + 1), one ballot, and the owner's word */
+    const auto owner = [&](uint32_t g) -> uint32_t {
+        const uint32_t gb = O + g;
+        if (tok && Ot - gb < CD_LANES) mark[Ot - gb] = gb + 1u;
+        cd_fence();
+        const uint64_t S = __ballot(mark[lane] == gb + 1u);
+        const uint32_t le = __builtin_amdgcn_mbcnt_hi((uint32_t)(S >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)S, 0u)) +
+                            (uint32_t)((S >> lane) & 1ull);
+        const uint32_t k = tbase + le - 1u;
+        tbase += (uint32_t)__builtin_popcountll(S);
+        return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)tinfo);
+    };
+#if CD_PIPEG
+    uint32_t tI = total ? owner(0u) : 0u;
+#endif
     for (uint32_t g = 0; g < total; g += CD_LANES) {
         const uint32_t gb = O + g;                     /* group's first output offset */
 #if CD_WHOLE
@@ -358,21 +385,23 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
             }
         }
 #endif
-        if (tok && Ot - gb < CD_LANES) mark[Ot - gb] = gb + 1u;
-        cd_fence();
-        const uint64_t S = __ballot(mark[lane] == gb + 1u);
-        const uint32_t le = __builtin_amdgcn_mbcnt_hi((uint32_t)(S >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)S, 0u)) +
-                            (uint32_t)((S >> lane) & 1ull);
-        const uint32_t k = tbase + le - 1u;
-        tbase += (uint32_t)__builtin_popcountll(S);
-        const uint32_t tInf = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)tinfo);
+#if CD_PIPEG
+        const uint32_t tInf = tI;
+#else
+        const uint32_t tInf = owner(g);
+#endif
         const uint32_t o = gb + lane;
         const uint32_t lit = (uint32_t)((int32_t)tInf >> 31);
         const uint32_t so = o - tInf;
         const uint32_t a = (((o + tInf) & imask) & lit) | ((outr_off + (so & omask)) & ~lit);
         const uint32_t q = so - gb;
         const uint32_t b = lds[a];
+#if CD_PIPEG
+        /* the next group's owners while this group's bytes are in flight (its
+         * byte reads come after this group's writes: one wave's LDS operations
+         * execute in order) */
+        const uint32_t tIn = g + CD_LANES < total ? owner(g + CD_LANES) : 0u;
+#endif
         uint32_t ent = (!lit && q < CD_LANES) ? (q << 8) : (0x10000u | b);
         while (__ballot(!(ent & 0x10000u)))
             ent = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((ent & 0x10000u) ? lane : (ent >> 8)) << 2), (int)ent);
@@ -381,6 +410,9 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
         if (g + CD_LANES <= total) dst[o] = (uint8_t)ent;
         else if (live) dst[o] = (uint8_t)ent;
         cd_fence();
+#if CD_PIPEG
+        tI = tIn;
+#endif
     }
 }
 
