@@ -350,6 +350,7 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
     const uint32_t tlen = (lane + 1u < ntok ? onext : O + total) - Ot;
     const bool whole_any = __ballot(tok && tlen >= CD_LANES && ((int32_t)tinfo < 0 || tinfo >= CD_LANES)) != 0ull;
 #endif
+#if CD_PIPEG
     /* the owner info of every byte of group g: marks of the token starts in
      * the group (tagged gb + 1), one ballot, and the owner's word */
     const auto owner = [&](uint32_t g) -> uint32_t {
@@ -364,7 +365,6 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
         tbase += (uint32_t)__builtin_popcountll(S);
         return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)tinfo);
     };
-#if CD_PIPEG
     uint32_t tI = total ? owner(0u) : 0u;
 #endif
     for (uint32_t g = 0; g < total; g += CD_LANES) {
@@ -388,7 +388,15 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
 #if CD_PIPEG
         const uint32_t tInf = tI;
 #else
-        const uint32_t tInf = owner(g);
+        if (tok && Ot - gb < CD_LANES) mark[Ot - gb] = gb + 1u;
+        cd_fence();
+        const uint64_t S = __ballot(mark[lane] == gb + 1u);
+        const uint32_t le = __builtin_amdgcn_mbcnt_hi((uint32_t)(S >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)S, 0u)) +
+                            (uint32_t)((S >> lane) & 1ull);
+        const uint32_t k = tbase + le - 1u;
+        tbase += (uint32_t)__builtin_popcountll(S);
+        const uint32_t tInf = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)tinfo);
 #endif
         const uint32_t o = gb + lane;
         const uint32_t lit = (uint32_t)((int32_t)tInf >> 31);
