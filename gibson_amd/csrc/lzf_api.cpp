@@ -38,7 +38,15 @@ int lzf_lds_order_check(void);      /* lzf_selfcheck.hip */
 
 namespace {
 
-enum KernelGen { GEN_TABLE = 0, GEN_LANE = 1, GEN_WINDOW = 2, GEN_SERIAL = 3, GEN_WTAB = 4 };
+enum KernelGen { GEN_TABLE = 0, GEN_LANE = 1, GEN_WINDOW = 2, GEN_SERIAL = 3, GEN_WTAB = 4, GEN_TABLE_ONLY = 5 };
+
+/* values of at most this many bytes take the lane generation by default
+ * (stream cand + lane parse), larger ones the table generation: json4k
+ * 1 M x 4 KiB 45.9 vs 48.7 ms (small class), text8k 1 M x 8 KiB 88.8 vs
+ * 111.0 ms (table), mixed16k 256 K x 16 KiB 65.1 vs 71.4 ms (table), but
+ * text64k 128 K x 64 KiB 127.4 vs 121.6 ms (the table's two-link records
+ * save the parse more hops than its cand costs) */
+constexpr uint32_t LANE_DEFAULT_MAX = 16384u;
 
 /* LZF_GPU_KERNEL picks the kernel generation, read per launch so one process
  * can A/B them.  Unset: the measured routing of launch_compress (the table
@@ -56,6 +64,7 @@ KernelGen kernel_gen()
     if (e && !strcmp(e, "window")) return GEN_WINDOW;
     if (e && !strcmp(e, "lane")) return GEN_LANE;
     if (e && !strcmp(e, "wtab")) return GEN_WTAB;
+    if (e && !strcmp(e, "table")) return GEN_TABLE_ONLY;
     return GEN_TABLE;
 }
 
@@ -249,18 +258,21 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
                    : lzf_launch_compress(b, s);
     case GEN_WTAB:
         return lzf_wtab_compress_supported(b.max_len) ? lane_compress(b, s, SU_WTAB) : lzf_launch_compress(b, s);
+    case GEN_TABLE_ONLY:
+        return (lzf_table_compress_supported(b.max_len) && b.count >= lane_min_count(b.max_len))
+                   ? lane_compress(b, s, SU_TABLE)
+                   : lzf_launch_compress(b, s);
     default:
         /* batches with values past 64 KiB, and small batches, go to the window
          * generation: the parse runs one value per lane, so its time has a
          * floor of one whole value's parse (~5 ms); below the crossover one
          * wave per value finishes first (tools/crossover.py).  Values of at
-         * most 4 KiB take the lane generation's small class (json4k: 56.7 vs
-         * 79.6 ms for the table's per-value 128 KiB table); past 4 KiB the
-         * table generation (text8k 145 vs 162 ms, mixed16k 329 vs 541 ms,
-         * text64k 262 vs 485 ms; profiles/r02/workloads.txt) */
+         * most LANE_DEFAULT_MAX bytes take the lane generation (the stream
+         * cand kernel, lzf_stream.hip, and the lane parse), larger ones the
+         * table generation (two-link records, lzf_cand.hip) */
         if (b.count < lane_min_count(b.max_len) || !lzf_table_compress_supported(b.max_len))
             return lzf_launch_compress(b, s);
-        return lane_compress(b, s, b.max_len > 4096u ? SU_TABLE : SU_LANE);
+        return lane_compress(b, s, b.max_len > LANE_DEFAULT_MAX ? SU_TABLE : SU_LANE);
     }
 }
 
@@ -900,8 +912,16 @@ const char *lzf_gpu_kernel_info(void)
         s = std::string("compress=wtab(cand_q1+wparse; window64 past 64 KiB) decompress=") +
             lzf_decompress_kernel_name();
         break;
+    case GEN_TABLE_ONLY:
+        s = std::string("compress=table(cand_table+parse_rec; window64 past 64 KiB or below ") +
+            std::to_string(lane_min_count(4096u)) + " values of <= 4 KiB / " +
+            std::to_string(lane_min_count(8192u)) + " of <= 8 KiB / " +
+            std::to_string(lane_min_count(16384u)) + " of <= 16 KiB / " +
+            std::to_string(lane_min_count(65536u)) + " of <= 64 KiB) decompress=" +
+            (lane_decoder() ? "lane" : lzf_decompress_kernel_name());
+        break;
     case GEN_LANE:
-        s = std::string("compress=lane(cand+parse; window64 past 64 KiB or below ") +
+        s = std::string("compress=lane(") + lzf_lane_cand_name() + "+parse_lane; window64 past 64 KiB or below " +
             std::to_string(lane_min_count(4096u)) + " values of <= 4 KiB / " +
             std::to_string(lane_min_count(8192u)) + " of <= 8 KiB / " +
             std::to_string(lane_min_count(16384u)) + " of <= 16 KiB / " +
@@ -909,7 +929,8 @@ const char *lzf_gpu_kernel_info(void)
             (lane_decoder() ? "lane" : lzf_decompress_kernel_name());
         break;
     default:
-        s = std::string("compress=table(cand_table+parse_rec; lane small class up to 4 KiB; window64 past 64 KiB or below ") +
+        s = std::string("compress=lane(") + lzf_lane_cand_name() + "+parse_lane) up to " +
+            std::to_string(LANE_DEFAULT_MAX / 1024u) + " KiB, table(cand_table+parse_rec) up to 64 KiB; window64 past 64 KiB or below " +
             std::to_string(lane_min_count(4096u)) + " values of <= 4 KiB / " +
             std::to_string(lane_min_count(8192u)) + " of <= 8 KiB / " +
             std::to_string(lane_min_count(16384u)) + " of <= 16 KiB / " +

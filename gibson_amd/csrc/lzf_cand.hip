@@ -39,6 +39,7 @@
  * Scratch per value: 4 B/position (records) + 1 bit/position (bitmap).
  */
 #include <stdlib.h>
+#include <string.h>
 
 #include "lzf_dev.h"
 
@@ -898,6 +899,11 @@ hipError_t lzf_launch_compress_table(const LzfBatch &b, hipStream_t s, void *scr
     /* diagnostics: LZF_GPU_TABLE_STAGE=1 runs kernel 1 only (its own time) */
     const char *stg = getenv("LZF_GPU_TABLE_STAGE");
     const bool cand_only = stg && *stg == '1';
+    /* kernel 1: the per-value pipeline (lzf_cand_table_kernel) or the stream
+     * form (lzf_stream.hip: values back to back, no per-value table clear
+     * or pipeline drain); LZF_GPU_TCAND=table|stream */
+    const char *tc = getenv("LZF_GPU_TCAND");
+    const bool stream = tc && !strcmp(tc, "stream");
     LzfRecScratch sc;
     sc.rec = (uint32_t *)scratch;
     sc.bits = (uint32_t *)((uint8_t *)scratch + ((chunk * rstride * 4u + 255u) & ~255ull));
@@ -920,8 +926,12 @@ hipError_t lzf_launch_compress_table(const LzfBatch &b, hipStream_t s, void *scr
         c.count = cnt;
         /* one 512-thread workgroup per CU (the table is 128 KiB), persistent */
         const uint32_t g = cnt < (uint32_t)cus ? cnt : (uint32_t)cus;
-        hipLaunchKernelGGL(lzf_cand_table_kernel, dim3(g), dim3(KT_THREADS), 0, s, c, sc);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (stream) {
+            if ((e = lzf_launch_cand_stream_rec(c, sc, s)) != hipSuccess) return e;
+        } else {
+            hipLaunchKernelGGL(lzf_cand_table_kernel, dim3(g), dim3(KT_THREADS), 0, s, c, sc);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
         if (cand_only) continue;
         hipLaunchKernelGGL(lzf_parse_rec_kernel, dim3((cnt + K3_THREADS - 1u) / K3_THREADS), dim3(K3_THREADS),
                            0, s, c, sc);

@@ -90,6 +90,9 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
                                     size_t scratch_bytes, uint32_t force_fix, hipStream_t aux,
                                     hipEvent_t *ev, uint32_t *chunks);
 size_t lzf_lane_scratch_per_value(uint32_t max_len);
+hipError_t lzf_launch_cand_stream(const LzfBatch &b, const LzfLaneScratch &sc, hipStream_t s);
+hipError_t lzf_launch_cand_stream_rec(const LzfBatch &b, const LzfRecScratch &sc, hipStream_t s);
+const char *lzf_lane_cand_name(void);
 bool lzf_lane_compress_supported(uint32_t max_len);
 hipError_t lzf_launch_compress(const LzfBatch &b, hipStream_t s);
 hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s);

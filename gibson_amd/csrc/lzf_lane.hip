@@ -37,6 +37,7 @@
  * Scratch per value: 2 B/position (cand) + 1 bit/position (bitmap).
  */
 #include <stdlib.h>
+#include <string.h>
 
 #include "lzf_internal.h"
 
@@ -1577,11 +1578,28 @@ static bool lane_ring_enabled()
 }
 #endif
 
+/* kernel 1 of the lane generation: the stream form (lzf_stream.hip: the
+ * exact table, values back to back in one pipeline per CU; any value of at
+ * most 64 KiB), or -- LZF_GPU_CAND=small, read per launch, a cross-check --
+ * the small class (values of at most 4 KiB; the diagnostic build's ring and
+ * mid classes past that).  json4k 1 M x 4 KiB: 45.9 ms with the stream form,
+ * 48.7 with the small class (cand 17.3 vs 19.9 ms, rocprof). */
+static bool lane_cand_small()
+{
+    const char *e = getenv("LZF_GPU_CAND");
+    return e && !strcmp(e, "small");
+}
+
+const char *lzf_lane_cand_name(void) { return lane_cand_small() ? "cand_small" : "cand_stream"; }
+
 bool lzf_lane_compress_supported(uint32_t max_len)
 {
 #ifndef LZF_DIAG
-    return max_len <= KS_MAXN;       /* the product library keeps the 4 KiB small class only */
+    /* the stream form takes any value the parse's 13-bit offsets and 16-bit
+     * positions cover; the small class values of at most 4 KiB */
+    return lane_cand_small() ? max_len <= KS_MAXN : max_len <= LZF_SLOTS;
 #else
+    if (!lane_cand_small()) return max_len <= LZF_SLOTS;
     if (max_len <= KS8_MAXN) return true;
     if (max_len <= KR64_MAXN && lane_ring_enabled()) return true;
     const char *e = getenv("LZF_GPU_LANE_MID");
@@ -1657,6 +1675,7 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)parse_lds);
         if (e != hipSuccess) return e;
     }
+    const bool stream = !lane_cand_small();
     hipError_t e;
     uint32_t i = 0;
     for (uint64_t first = 0; first < b.count; first += chunk, i++) {
@@ -1671,7 +1690,9 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
         c.count = cnt;
         /* scratch half h is free once kernel 2 of chunk i-2 is done */
         if (pipe && i >= 2u && (e = hipStreamWaitEvent(s, ev[2 + h], 0)) != hipSuccess) return e;
-        if (b.max_len <= KS_MAXN) {
+        if (stream) {
+            if ((e = lzf_launch_cand_stream(c, sc[h], s)) != hipSuccess) return e;
+        } else if (b.max_len <= KS_MAXN) {
             const uint32_t g = cnt < small_grid ? cnt : small_grid;
             hipLaunchKernelGGL((lzf_cand_small_kernel<4u, KS_MAXN, KS_WIN>), dim3(g), dim3(64), 0, s, c, sc[h]);
         }

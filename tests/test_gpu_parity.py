@@ -18,8 +18,20 @@ from tests.oracle_lib import sha16, synth
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-GENERATIONS = ["table", "wtab", "lane", "window", "serial", "lane-diag"]
+# "default": the library's routing (lane generation with the stream cand
+# kernel up to 16 KiB, table generation to 64 KiB); the rest forced
+GENERATIONS = ["default", "table", "wtab", "lane", "lane-small", "window", "serial", "lane-diag"]
 DIAG = {"serial", "lane-diag"}      # cross-check forms: the diagnostic build only
+GEN_ENV = {
+    "default": {},
+    "table": {"LZF_GPU_KERNEL": "table"},
+    "wtab": {"LZF_GPU_KERNEL": "wtab"},
+    "lane": {"LZF_GPU_KERNEL": "lane"},                              # stream cand kernel
+    "lane-small": {"LZF_GPU_KERNEL": "lane", "LZF_GPU_CAND": "small"},  # small class (<= 4 KiB)
+    "window": {"LZF_GPU_KERNEL": "window"},
+    "serial": {"LZF_GPU_KERNEL": "serial"},
+    "lane-diag": {"LZF_GPU_KERNEL": "lane", "LZF_GPU_CAND": "small"},   # diag: small/ring classes
+}
 
 
 @pytest.fixture(autouse=True)
@@ -49,10 +61,10 @@ def diag():
 @pytest.fixture(params=GENERATIONS)
 def generation(request, monkeypatch):
     gen = request.param
-    if gen == "table":
-        monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
-    else:
-        monkeypatch.setenv("LZF_GPU_KERNEL", gen.replace("-diag", ""))
+    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.delenv("LZF_GPU_CAND", raising=False)
+    for k, v in GEN_ENV[gen].items():
+        monkeypatch.setenv(k, v)
     if gen in DIAG:
         with _diag():
             yield gen
@@ -254,6 +266,7 @@ def test_lane_mid_class(oracle, monkeypatch, diag):
     # the mid-class lane kernels (values 4 KiB .. 64 KiB), opt-in
     from tests.gpu_batch import gpu_compress
     monkeypatch.setenv("LZF_GPU_KERNEL", "lane")
+    monkeypatch.setenv("LZF_GPU_CAND", "small")
     monkeypatch.setenv("LZF_GPU_LANE_MID", "1")
     monkeypatch.setenv("LZF_GPU_LANE_RING", "0")
     rnd = random.Random(21)
@@ -269,6 +282,7 @@ def test_lane_ring_class(oracle, monkeypatch, align, diag):
     # 16 KiB the bytes streamed through an LDS ring
     from tests.gpu_batch import gpu_compress, gpu_decompress
     monkeypatch.setenv("LZF_GPU_KERNEL", "lane")
+    monkeypatch.setenv("LZF_GPU_CAND", "small")
     monkeypatch.setenv("LZF_GPU_LANE_RING", "1")
     rnd = random.Random(33 + align)
     vals = []
@@ -289,12 +303,14 @@ def test_lane_ring_class(oracle, monkeypatch, align, diag):
 
 
 @pytest.mark.parametrize("nmax", [4096, 8192, 16384, 65536])
-def test_lane_scratch_chunks(oracle, monkeypatch, nmax, diag):
+@pytest.mark.parametrize("cand", ["stream", "small"])
+def test_lane_scratch_chunks(oracle, monkeypatch, nmax, cand, diag):
     # a small compress scratch cap runs the lane kernels over many chunks;
     # the scratch is per host thread, so a fresh thread sees the cap
     import threading
     from tests.gpu_batch import gpu_compress
     monkeypatch.setenv("LZF_GPU_KERNEL", "lane")
+    monkeypatch.setenv("LZF_GPU_CAND", cand)
     monkeypatch.setenv("LZF_GPU_SCRATCH_MB", "4")
     rnd = random.Random(nmax)
     vals = [synth(rnd.randrange(6), 0x5EED00FA, i, rnd.randint(1, nmax)) for i in range(400)]
@@ -312,7 +328,7 @@ def test_table_scratch_chunks(oracle, monkeypatch, nmax):
     # host thread: the scratch is per host thread)
     import threading
     from tests.gpu_batch import gpu_compress
-    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.setenv("LZF_GPU_KERNEL", "table")
     monkeypatch.setenv("LZF_GPU_SCRATCH_MB", "4")
     rnd = random.Random(nmax + 1)
     vals = [synth(rnd.randrange(6), 0x5EED00FB, i, rnd.randint(1, nmax)) for i in range(300)]
@@ -330,6 +346,7 @@ def test_wave_parse(oracle, monkeypatch, align, diag):
     # every size class edge of a window, caps that run out inside a window
     from tests.gpu_batch import gpu_compress
     monkeypatch.setenv("LZF_GPU_KERNEL", "lane")
+    monkeypatch.setenv("LZF_GPU_CAND", "small")
     monkeypatch.setenv("LZF_GPU_LANE_PARSE", "wave")
     rnd = random.Random(77 + align)
     vals = [synth(rnd.randrange(6), 0x5EED00E0, i, rnd.randint(1, 4096)) for i in range(400)]
@@ -356,6 +373,7 @@ def test_lane_order_repair_path(oracle, monkeypatch, diag):
     # streams
     from tests.gpu_batch import gpu_compress
     monkeypatch.setenv("LZF_GPU_KERNEL", "lane")
+    monkeypatch.setenv("LZF_GPU_CAND", "small")
     monkeypatch.setenv("LZF_GPU_LANE_FORCE_FIX", "1")
     monkeypatch.setenv("LZF_GPU_LANE_MID", "1")
     monkeypatch.setenv("LZF_GPU_LANE_RING", "0")
@@ -453,12 +471,12 @@ CONFIGS = [
     # value is checked against the reference's digest (tests/golden/digests.json)
     (1, 0x5EED0002, 4096, 65536),
     (2, 0x5EED0003, 65536, 65536),
-    (2, 0x5EED0003, 65536, 262144),
-    (0, 0x5EED0004, 8192, 65536),   # the table generation (values past 4 KiB)
+    (2, 0x5EED0003, 65536, 262144),  # the table generation (values past 16 KiB)
+    (0, 0x5EED0004, 8192, 65536),
     (3, 0x5EED0005, 16384, 65536),
     # the production routes at the configs' real per-GPU counts: 262 144
-    # values of 4 KiB run the lane small class, 131 072 of 16 KiB the table
-    # generation (below 163 840 / 81 920 values both would run window64)
+    # values of 4 KiB and 131 072 of 16 KiB run the lane generation with the
+    # stream cand kernel (below 163 840 / 81 920 values both would run window64)
     (1, 0x5EED0002, 4096, 262144),
     (3, 0x5EED0005, 16384, 131072),
 ]
@@ -474,6 +492,19 @@ def digests():
 @pytest.mark.parametrize("kind,seed,n,count", CONFIGS)
 def test_full_batch_digest_and_roundtrip(kind, seed, n, count, digests, monkeypatch):
     monkeypatch.delenv("LZF_GPU_LANE_MIN", raising=False)      # the routing the bench uses
+    _digest_case(kind, seed, n, count, digests)
+
+
+@pytest.mark.parametrize("kind,seed,n,count", [c for c in CONFIGS if c[2] <= 16384 and c[3] >= 131072])
+@pytest.mark.parametrize("gen", ["table", "lane-small"])
+def test_full_batch_digest_other_cand(kind, seed, n, count, gen, digests, monkeypatch):
+    # the production-size digests through the generations the routing no
+    # longer takes there: the table generation, and (4 KiB) the small class
+    if gen == "lane-small" and n > 4096:
+        pytest.skip("the small class takes values of at most 4 KiB")
+    monkeypatch.delenv("LZF_GPU_LANE_MIN", raising=False)
+    for k, v in GEN_ENV[gen].items():
+        monkeypatch.setenv(k, v)
     _digest_case(kind, seed, n, count, digests)
 
 
