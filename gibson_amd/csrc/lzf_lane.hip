@@ -1676,6 +1676,9 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
         if (e != hipSuccess) return e;
     }
     const bool stream = !lane_cand_small();
+    /* diagnostics: LZF_GPU_LANE_STAGE=1 runs kernel 1 only (its own time) */
+    const char *stg = getenv("LZF_GPU_LANE_STAGE");
+    const bool cand_only = stg && *stg == '1';
     hipError_t e;
     uint32_t i = 0;
     for (uint64_t first = 0; first < b.count; first += chunk, i++) {
@@ -1711,6 +1714,7 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
         }
 #endif
         if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (cand_only) continue;
         hipStream_t s2 = s;
         if (pipe) {
             if ((e = hipEventRecord(ev[h], s)) != hipSuccess) return e;

@@ -316,7 +316,12 @@ __global__ __launch_bounds__(KS_THR) void lzf_cand_stream_kernel(LzfBatch bt, ui
                         xd[i] = e.y;
                     }
                 }
+#ifdef KS_ABL_B     /* diagnostics: no exchanges (outputs wrong) */
+#pragma unroll
+                for (uint32_t i = 0; i < 15u; i++) xr[i] = xd[i];
+#else
                 ks_xchg15(xr, xa, xm, xd);
+#endif
 #pragma unroll
                 for (uint32_t i = 0; i < 15u; i++) Ok[64u * i + lane] = (uint16_t)(xr[i] >> hs[i]);
             }
@@ -417,6 +422,9 @@ __global__ __launch_bounds__(KS_THR) void lzf_cand_stream_kernel(LzfBatch bt, ui
         }
         /* ---- the step's loads, every wave: the agreement bytes of C1, then
          * the window of block t + KS_PF --------------------------------------- */
+#ifdef KS_ABL_LD     /* diagnostics: the agreement load at p's own line (outputs wrong) */
+        lq = pw[PS].lb + lane;
+#endif
         c_b[CS] = ks_ld(lsrc, ln, lq);
         if constexpr (REC) c_b2[CS] = ks_ld(lsrc, ln, lq2);
         pw[PS] = window_or_none(KS_WINS * (t + KS_PF) + jj);

@@ -20,11 +20,12 @@ pytestmark = pytest.mark.gpu
 
 # "default": the library's routing (lane generation with the stream cand
 # kernel up to 16 KiB, table generation to 64 KiB); the rest forced
-GENERATIONS = ["default", "table", "wtab", "lane", "lane-small", "window", "serial", "lane-diag"]
+GENERATIONS = ["default", "table", "table-stream", "wtab", "lane", "lane-small", "window", "serial", "lane-diag"]
 DIAG = {"serial", "lane-diag"}      # cross-check forms: the diagnostic build only
 GEN_ENV = {
     "default": {},
     "table": {"LZF_GPU_KERNEL": "table"},
+    "table-stream": {"LZF_GPU_KERNEL": "table", "LZF_GPU_TCAND": "stream"},   # records from the stream kernel
     "wtab": {"LZF_GPU_KERNEL": "wtab"},
     "lane": {"LZF_GPU_KERNEL": "lane"},                              # stream cand kernel
     "lane-small": {"LZF_GPU_KERNEL": "lane", "LZF_GPU_CAND": "small"},  # small class (<= 4 KiB)
@@ -63,6 +64,7 @@ def generation(request, monkeypatch):
     gen = request.param
     monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
     monkeypatch.delenv("LZF_GPU_CAND", raising=False)
+    monkeypatch.delenv("LZF_GPU_TCAND", raising=False)
     for k, v in GEN_ENV[gen].items():
         monkeypatch.setenv(k, v)
     if gen in DIAG:
