@@ -33,6 +33,9 @@
 #define KS_THR    (64u * (KS_WINS + 1u))
 #define KS_PF     4u                         /* blocks of input in flight (the step loop's unroll) */
 #define KS_CL     2u                         /* steps from the agreement load to its use */
+#ifndef KS_OPT
+#define KS_OPT    1                          /* byte shifts only near a value's end; p's slot carried from A to C2 */
+#endif
 
 __device__ __forceinline__ uint32_t ks_lds_addr(const void *p)
 {
@@ -130,6 +133,28 @@ __device__ __forceinline__ uint2 ks_fix(uint2 v, uint32_t n, uint32_t pp)
 }
 
 template <uint32_t V> struct KsIc { static constexpr uint32_t value = V; };
+
+/* -DKS_TIMING (diagnostic builds): cycles per phase summed over waves in
+ * ks_times[]: [0] table wave B, [1] table wave loads, [2] table wave
+ * barrier, [3] C2, [4] C1 (with Q), [5] A, [6] worker loads + cursor,
+ * [7] worker barrier, [8] steps (every wave) */
+#ifdef KS_TIMING
+__device__ unsigned long long ks_times[16];
+extern "C" int lzf_gpu_debug_ks(unsigned long long *out16, int reset)
+{
+    hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(ks_times), sizeof(ks_times));
+    if (e == hipSuccess && reset) {
+        unsigned long long z[16] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(ks_times), z, sizeof(z));
+    }
+    return e == hipSuccess ? 0 : -2;
+}
+#define KS_T0() uint64_t ks_t = __builtin_amdgcn_s_memtime()
+#define KS_TM(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); ks_acc[i] += t_ - ks_t; ks_t = t_; } while (0)
+#else
+#define KS_T0() ((void)0)
+#define KS_TM(i) ((void)0)
+#endif
 
 /* agreement code of k equal bytes (src/lzf_c.c:151-158 and the parse's
  * walk): 1 differ within 3, 2..6 exactly k (3..7), 7 at least 8 */
@@ -264,6 +289,7 @@ __global__ __launch_bounds__(KS_THR) void lzf_cand_stream_kernel(LzfBatch bt, ui
     noff = cin_off[nv];
     KsWin pw[KS_PF];
     uint2 pa[KS_PF], aa[KS_PF];
+    [[maybe_unused]] uint32_t as_[KS_PF] = {0u, 0u, 0u, 0u};   /* slot of p, with aa (KS_OPT) */
 #pragma unroll
     for (uint32_t s = 0; s < KS_PF; s++) {
         pw[s] = window_or_none(KS_WINS * s + jj);
@@ -274,6 +300,7 @@ __global__ __launch_bounds__(KS_THR) void lzf_cand_stream_kernel(LzfBatch bt, ui
     uint32_t c_v[KS_CL], c_n[KS_CL];
     uint32_t c_p[KS_CL], c_q[KS_CL], c_q2[KS_CL];
     uint2 c_a[KS_CL], c_b[KS_CL], c_b2[KS_CL];
+    [[maybe_unused]] uint32_t c_s[KS_CL] = {0u, 0u};
 #pragma unroll
     for (uint32_t i = 0; i < KS_CL; i++) {
         c_v[i] = c_n[i] = 0u;
@@ -283,10 +310,14 @@ __global__ __launch_bounds__(KS_THR) void lzf_cand_stream_kernel(LzfBatch bt, ui
     }
     const uint32_t tb = ks_lds_addr(T);
 
+#ifdef KS_TIMING
+    uint64_t ks_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     const auto step = [&](auto ps, uint32_t t) {
         constexpr uint32_t PS = decltype(ps)::value;             /* t % KS_PF */
         constexpr uint32_t CS = PS % KS_CL;
         constexpr uint32_t S2 = (PS + KS_PF - 2u) % KS_PF;        /* block t-2 */
+        KS_T0();
         /* the agreement loads' addresses: a harmless default inside block t's
          * value, replaced by C1's candidates */
         const uint8_t *lsrc = ks_src(bt, pw[PS]);
@@ -325,34 +356,42 @@ __global__ __launch_bounds__(KS_THR) void lzf_cand_stream_kernel(LzfBatch bt, ui
 #pragma unroll
                 for (uint32_t i = 0; i < 15u; i++) Ok[64u * i + lane] = (uint16_t)(xr[i] >> hs[i]);
             }
+            KS_TM(0);
         } else {
             /* ---- C2(t-2-KS_CL): slot tests, agreements, the output -------- */
             if (c_p[CS] != 0xFFFFFFFFu) {
                 const uint32_t p = c_p[CS], q = c_q[CS], n = c_n[CS];
-                const uint2 a = c_a[CS], b = ks_fix(c_b[CS], n, q);
+                const uint2 a = c_a[CS];
+#if KS_OPT
+                /* no lane within 8 bytes of its value's end: every q < p too,
+                 * so the loads were not moved back and need no shift */
+                const bool near_end = __ballot(p + 8u > n) != 0ull;
+                const uint2 b = near_end ? ks_fix(c_b[CS], n, q) : c_b[CS];
+                const uint32_t sp = c_s[CS];
+#else
+                const bool near_end = true;
+                const uint2 b = ks_fix(c_b[CS], n, q);
                 const uint32_t sp = dv_slot(a.x);
-                uint32_t word = 0u;
-                /* q1: a stale table entry names a position of another slot */
-                if (q != 0u) {
-                    const uint32_t k1 = ks_agree(a, b, n - p);
-                    if (k1 >= 3u || dv_slot(b.x) == sp) {
-                        word = (ks_code(k1) << 13) | (p - q - 1u);
-                        if constexpr (REC) {
-                            const uint32_t q2 = c_q2[CS];
-                            const uint2 b2 = ks_fix(c_b2[CS], n, q2);
-                            if (q2 != 0u) {
-                                const uint32_t k2 = ks_agree(a, b2, n - p);
-                                if (k2 >= 3u || dv_slot(b2.x) == sp)
-                                    word |= ((ks_code(k2) << 13) | (p - q2 - 1u)) << 16;
-                            }
-                        }
-                    }
+#endif
+                /* branch-free (every branch costs the wave its exec-mask
+                 * juggling): both tests always, the word by selects.  q1: a
+                 * stale table entry names a position of another slot */
+                const uint32_t k1 = ks_agree(a, b, n - p);
+                const bool v1 = q != 0u && (k1 >= 3u || dv_slot(b.x) == sp);
+                uint32_t word = v1 ? (ks_code(k1) << 13) | (p - q - 1u) : 0u;
+                if constexpr (REC) {
+                    const uint32_t q2 = c_q2[CS];
+                    const uint2 b2 = near_end ? ks_fix(c_b2[CS], n, q2) : c_b2[CS];
+                    const uint32_t k2 = ks_agree(a, b2, n - p);
+                    const bool v2 = v1 && q2 != 0u && (k2 >= 3u || dv_slot(b2.x) == sp);
+                    word |= v2 ? ((ks_code(k2) << 13) | (p - q2 - 1u)) << 16 : 0u;
                 }
                 if constexpr (REC)
                     ((uint32_t *)out)[(uint64_t)c_v[CS] * ostride + p] = word;
                 else
                     ((uint16_t *)out)[(uint64_t)c_v[CS] * ostride + p] = (uint16_t)word;
             }
+            KS_TM(3);
             /* ---- REC: Q <- O of block t-3 ------------------------------ */
             if constexpr (REC) {
                 if (t >= 3u && t - 3u < nb) {
@@ -378,6 +417,9 @@ __global__ __launch_bounds__(KS_THR) void lzf_cand_stream_kernel(LzfBatch bt, ui
                     c_p[CS] = p;
                     c_q[CS] = ok ? qg - dg0 : 0u;
                     c_a[CS] = aa[S2];
+#if KS_OPT
+                    c_s[CS] = as_[S2];
+#endif
                     lq = ok ? qg - dg0 : p;
                     if constexpr (REC) {
                         /* q1's own old entry: block t-2 or t-3 in O, else Q */
@@ -397,18 +439,24 @@ __global__ __launch_bounds__(KS_THR) void lzf_cand_stream_kernel(LzfBatch bt, ui
                 lsrc = dsrc;
                 ln = dn;
             }
+            KS_TM(4);
             /* ---- A(t): slots of the worker's window of block t ------------ */
             if (t < nb) {
                 const KsWin &d = pw[PS];
                 const uint32_t p = d.lb + lane;
                 const bool act = d.live && p < d.n - 2u;
+#if KS_OPT
+                const uint2 pb = d.lb + 64u + 8u <= d.n ? pa[PS] : ks_fix(pa[PS], d.n, p);
+#else
                 const uint2 pb = ks_fix(pa[PS], d.n, p);
+#endif
+                const uint32_t sl = dv_slot(pb.x);
                 if constexpr (REC) {
                     /* the stream position of this lane is the block's (the
                      * table wave's data), which is d.g0 + p for a live lane */
-                    S[KS_BLK * (t & 1u) + 64u * j + lane] = act ? (dv_slot(pb.x) | (1u << 16)) : 0u;
+                    S[KS_BLK * (t & 1u) + 64u * j + lane] = act ? (sl | (1u << 16)) : 0u;
                 } else {
-                    const uint32_t h = act ? dv_slot(pb.x) : LZF_SLOTS + lane;
+                    const uint32_t h = act ? sl : LZF_SLOTS + lane;
                     const uint32_t data = act ? ((d.g0 + p) & 0xFFFFu) : 0u;
                     S[KS_BLK * (t & 1u) + 64u * j + lane] =
                         make_uint2((tb + 4u * (h >> 1)) | (h & 1u), data << ((h & 1u) << 4));
@@ -418,7 +466,11 @@ __global__ __launch_bounds__(KS_THR) void lzf_cand_stream_kernel(LzfBatch bt, ui
                     *(uint4 *)&D[PS][j][4] = make_uint4(d.lb, d.g0, d.live, 0u);
                 }
                 aa[PS] = pb;
+#if KS_OPT
+                as_[PS] = sl;
+#endif
             }
+            KS_TM(5);
         }
         /* ---- the step's loads, every wave: the agreement bytes of C1, then
          * the window of block t + KS_PF --------------------------------------- */
@@ -429,7 +481,14 @@ __global__ __launch_bounds__(KS_THR) void lzf_cand_stream_kernel(LzfBatch bt, ui
         if constexpr (REC) c_b2[CS] = ks_ld(lsrc, ln, lq2);
         pw[PS] = window_or_none(KS_WINS * (t + KS_PF) + jj);
         pa[PS] = ks_ld(ks_src(bt, pw[PS]), pw[PS].n, pw[PS].lb + lane);
+        if (w) KS_TM(6);
+        else KS_TM(1);
         __syncthreads();
+        if (w) KS_TM(7);
+        else KS_TM(2);
+#ifdef KS_TIMING
+        ks_acc[8]++;
+#endif
     };
     for (uint32_t t = 0; t < nb + 2u + KS_CL; t += KS_PF) {
         step(KsIc<0>{}, t);
@@ -437,6 +496,10 @@ __global__ __launch_bounds__(KS_THR) void lzf_cand_stream_kernel(LzfBatch bt, ui
         step(KsIc<2>{}, t + 2u);
         step(KsIc<3>{}, t + 3u);
     }
+#ifdef KS_TIMING
+    if (lane == 0u)
+        for (uint32_t i = 0; i < 9u; i++) atomicAdd(&ks_times[i], (unsigned long long)ks_acc[i]);
+#endif
 }
 static_assert(KS_PF == 4u && KS_CL == 2u, "the step loop is unrolled 4x; C2 runs KS_CL steps after C1");
 
