@@ -391,6 +391,12 @@ __global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt,
 #ifndef K3_RW
 #define K3_RW      32u          /* bitmap words kept in LDS per lane (power of two) */
 #endif
+#ifndef K3_LITMIN
+#define K3_LITMIN   8u       /* lanes of the wave that must take a free-literal trip for it to run */
+#endif
+#ifndef K3_LITX
+#define K3_LITX    3u           /* free literals taken after a literal in the same iteration (0: none) */
+#endif
 
 /* rel codes of the walk, relative to p: the record codes 0..7, plus
  * 8 (the first 3 bytes agree, length unknown) and 9 (unknown) */
@@ -743,6 +749,51 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
                         curw = 0u;
                     }
                     mode = K3_STEP;
+#if K3_LITX
+                    /* free literals (lzf_lane.hip's parse has the same path):
+                     * positions whose record has no candidate at all (code1
+                     * 0, src/lzf_c.c:153-158), with the record and the byte in
+                     * registers, up to K3_LITX more per iteration */
+                    /* only when enough lanes of the wave are at a literal at
+                     * all (one ballot of the branch's lanes): on text, where
+                     * few are, the wave skips the path */
+                    bool go = true;
+                    if ((uint32_t)__builtin_popcountll(__ballot(true)) >= K3_LITMIN)
+#pragma unroll
+                    for (uint32_t e_ = 0; e_ < K3_LITX; e_++) {
+                        const uint32_t d_ = p - cb, x_ = p - wb;
+                        go = go && p < n - 2u && d_ < K3_CB && x_ < 16u && o < cap;
+                        if (go) {
+                            const bool b0_ = d_ & 1u, b1_ = d_ & 2u;
+                            const uint32_t c0_ = b1_ ? (b0_ ? C0.w : C0.z) : (b0_ ? C0.y : C0.x);
+                            const uint32_t c1_ = b1_ ? (b0_ ? C1.w : C1.z) : (b0_ ? C1.y : C1.x);
+                            const uint32_t c2_ = b1_ ? (b0_ ? C2.w : C2.z) : (b0_ ? C2.y : C2.x);
+                            const uint32_t c3_ = b1_ ? (b0_ ? C3.w : C3.z) : (b0_ ? C3.y : C3.x);
+                            const uint32_t c_ = (d_ & 8u) ? ((d_ & 4u) ? c3_ : c2_) : ((d_ & 4u) ? c1_ : c0_);
+                            go = (c_ & 0xE000u) == 0u;
+                        }
+                        /* a trip the wave takes only when enough lanes gain
+                         * from it: on text, where few do, the others would
+                         * wait through it */
+                        if ((uint32_t)__builtin_popcountll(__ballot(go)) < K3_LITMIN) break;
+                        if (go) {
+                            curw |= 1u << (p & 31u);
+                            const uint32_t byte_ = (dv_sel4(W, x_ >> 2) >> (8u * (x_ & 3u))) & 0xFFu;
+                            const bool first_ = run == 0u;
+                            hx = first_ ? 4u * fw + accn : hx;
+                            K3_PUT(first_ ? byte_ << 8 : byte_, first_ ? 2u : 1u);
+                            o++;
+                            if (++run == LZF_MAX_LIT) { K3_PATCH(hx, LZF_MAX_LIT - 1u); run = 0u; o++; }
+                            p++;
+                            if ((p & 31u) == 0u) {
+                                K3_FLUSH_TO(cw);
+                                K3_RING(cw) = curw;
+                                cw++;
+                                curw = 0u;
+                            }
+                        }
+                    }
+#endif
                 }
             } else {
                 uint32_t maxlen = n - p - 2u;                            /* src/lzf_c.c:169-170 */

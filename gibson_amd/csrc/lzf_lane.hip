@@ -931,6 +931,12 @@ extern "C" int lzf_gpu_debug_sites(unsigned long long *out16, int reset)
 #ifndef K2_NRES
 #define K2_NRES 1u
 #endif
+#ifndef K2_LITMIN
+#define K2_LITMIN   8u       /* lanes of the wave that must take a free-literal trip for it to run */
+#endif
+#ifndef K2_LITX
+#define K2_LITX 3u       /* free literals taken after a literal in the same iteration (0: none) */
+#endif
 enum { K2_STEP = 0, K2_RESOLVE = 1, K2_DECIDE = 2, K2_EXTEND = 3, K2_EMIT = 4, K2_DONE = 5 };
 
 __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt, LzfLaneScratch sc)
@@ -1145,6 +1151,50 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                         curw = 0u;
                     }
                     mode = K2_STEP;
+#if K2_LITX
+                    /* free literals: while the next positions have no
+                     * candidate at all (cand code 0: no earlier position with
+                     * their slot in the window, so no inserted one either,
+                     * src/lzf_c.c:153-158), and their cand word and byte are
+                     * already in registers, they are literals with no memory
+                     * access -- up to K2_LITX more per iteration */
+                    /* only when enough lanes of the wave are at a literal at
+                     * all (one ballot of the branch's lanes): on text, where
+                     * few are, the wave skips the path */
+                    bool go = true;
+                    if ((uint32_t)__builtin_popcountll(__ballot(true)) >= K2_LITMIN)
+#pragma unroll
+                    for (uint32_t e_ = 0; e_ < K2_LITX; e_++) {
+                        const uint32_t d_ = p - cb, x_ = p - wb;
+                        go = go && p < n - 2u && d_ < K2_CB && x_ < 16u && o < cap;
+                        if (go) {
+                            const uint32_t dw_ = d_ >> 1;
+                            const uint4 Cq_ = dw_ < 8u ? (dw_ < 4u ? C0 : C1) : (dw_ < 12u ? C2 : C3);
+                            go = ((ln_sel4(Cq_, dw_ & 3u) >> (16u * (d_ & 1u))) & 0xE000u) == 0u;
+                        }
+                        /* a trip the wave takes only when enough lanes gain
+                         * from it: on text, where few do, the others would
+                         * wait through it */
+                        if ((uint32_t)__builtin_popcountll(__ballot(go)) < K2_LITMIN) break;
+                        if (go) {
+                            K2_SITE(9);
+                            curw |= 1u << (p & 31u);
+                            const uint32_t byte_ = (ln_sel4(W, x_ >> 2) >> (8u * (x_ & 3u))) & 0xFFu;
+                            const bool first_ = run == 0u;
+                            hx = first_ ? 4u * fw + accn : hx;
+                            K2_PUT(first_ ? byte_ << 8 : byte_, first_ ? 2u : 1u);
+                            o++;
+                            if (++run == LZF_MAX_LIT) { K2_PATCH(hx, LZF_MAX_LIT - 1u); run = 0u; o++; }
+                            p++;
+                            if ((p & 31u) == 0u) {
+                                K2_FLUSH_TO(cw);
+                                K2_RING(cw) = curw;
+                                cw++;
+                                curw = 0u;
+                            }
+                        }
+                    }
+#endif
                 }
             } else {
                 uint32_t maxlen = n - p - 2u;                            /* src/lzf_c.c:169-170 */
