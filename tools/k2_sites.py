@@ -9,6 +9,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ["LZF_HIP_LIB"] = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gibson_amd",
                                          "liblzf_hip_sites.so")
 os.environ["LZF_GPU_LANE_PIPE"] = "0"
+os.environ.setdefault("LZF_GPU_LANE_MIN", "0")   # the lane route at any batch size
 import torch  # noqa: E402
 
 import gibson_amd  # noqa: E402
@@ -31,7 +32,7 @@ gibson_amd.compress_batch(src, off, ln, out, off, cap, olen, n)
 torch.cuda.synchronize()
 L.lzf_gpu_debug_sites(buf, 0)
 names = ["lane-iterations", "C load", "C2 use", "bits load", "walk cand load", "eq3", "input window",
-         "extend piece", "out dword", "wave: walk stops", "steps", "wave: windows", "wave: walk hops",
+         "extend piece", "out dword", "free literal | wave: walk stops", "steps", "wave: windows", "wave: walk hops",
          "wave: long measures", "wave: truncations", "wave: orbit stops"]
 for i, nm in enumerate(names):
     if nm != "-":
