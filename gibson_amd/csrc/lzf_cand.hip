@@ -391,6 +391,9 @@ __global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt,
 #ifndef K3_RW
 #define K3_RW      32u          /* bitmap words kept in LDS per lane (power of two) */
 #endif
+#ifndef K3_NOSTORE
+#define K3_NOSTORE 0        /* diagnostic: 1 = the output's 16-byte stores are skipped (timing only) */
+#endif
 #ifndef K3_LITMIN
 #define K3_LITMIN   8u       /* lanes of the wave that must take a free-literal trip for it to run */
 #endif
@@ -555,7 +558,8 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
             __builtin_memcpy(da + 12u, &l_, 4);                                    \
         } else {                                                                   \
             const uint4 v_ = make_uint4(pb0, pb1, pb2, (w_));                      \
-            __builtin_memcpy(da + 4u * fs, &v_, 16);                               \
+            if (!K3_NOSTORE || bt.max_len == 0xFFFFFFFFu)                          \
+                __builtin_memcpy(da + 4u * fs, &v_, 16);                           \
         }                                                                          \
     } while (0)
 #define K3_PUT(bytes_, cnt_)                                                       \

@@ -77,6 +77,12 @@
 #define CD_PIPEG   0
 #endif
 static_assert(!(CD_WHOLE && CD_PIPEG), "the whole-token path keeps tbase per group");
+/* step 4's stores: 1 = completed output leaves the LDS window in 16-byte
+ * pieces per lane, a flush unit (1 KiB, or half the window) at a time; 0 =
+ * one global byte store per lane per 64-byte group */
+#ifndef CD_WIDE
+#define CD_WIDE    1
+#endif
 /* decoder form: 1 = pipe (producer + consumer wave per stream), 0 = tokpar64 */
 #ifndef CD_PIPE
 #define CD_PIPE    1
@@ -315,6 +321,27 @@ __device__ __forceinline__ CdRound cd_decode(const uint8_t *inr, uint32_t imask,
     return r;
 }
 
+/* output bytes [F, E) of the LDS window (ring offset outr_off, mask omask)
+ * to dst: 16 bytes per lane, at most `unit` bytes per pass (unit <= 1024,
+ * a multiple of 16), then the last < 16 bytes one per lane.  The window
+ * still holds every byte of [F, E): E - F stays below half the window */
+__device__ __forceinline__ void cd_flush(const uint8_t *lds, uint32_t outr_off, uint32_t omask, uint8_t *dst,
+                                         uint32_t &F, uint32_t E, uint32_t lane)
+{
+    while (E - F >= 16u) {
+        const uint32_t x = F + 16u * lane;
+        if (x + 16u <= E) {
+            uint4 v;
+            __builtin_memcpy(&v, lds + outr_off + (x & omask), 16);
+            __builtin_memcpy(dst + x, &v, 16);
+        }
+        const uint32_t nfull = (E - F) & ~15u;
+        F += nfull < 16u * CD_LANES ? nfull : 16u * CD_LANES;
+    }
+    if (F + lane < E) dst[F + lane] = lds[outr_off + ((F + lane) & omask)];
+    F = E;
+}
+
 /* step 4: the round's output [O, O + total), 64 bytes per step.  Tokens sit
  * in lanes in output order, so the owner of output byte b of a group is
  * (tokens started before the group) + (token starts in the group at or below
@@ -331,8 +358,16 @@ __device__ __forceinline__ CdRound cd_decode(const uint8_t *inr, uint32_t imask,
 template <uint32_t IN_RING>
 __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint32_t omask, uint32_t *mark,
                                              uint32_t sink_off, uint8_t *dst, uint32_t O, uint32_t total, bool tok,
-                                             uint32_t Ot, uint32_t tinfo, uint32_t lane)
+                                             uint32_t Ot, uint32_t tinfo, uint32_t lane, uint32_t &F)
 {
+    /* CD_WIDE: a flush unit of the window's completed bytes goes out as soon
+     * as it is complete (half the window at most, so no byte is overwritten
+     * before it is stored) */
+#if CD_WIDE
+    const uint32_t unit = (omask + 1u) / 2u < 1024u ? (omask + 1u) / 2u : 1024u;
+#else
+    (void)F;
+#endif
     constexpr uint32_t imask = IN_RING - 1u;
     uint32_t tbase = 0;          /* tokens started before the group */
 #ifdef LZF_CD_ABLATE_OUTPUT           /* diagnostic builds only: time discovery alone */
@@ -415,9 +450,26 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
             ent = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((ent & 0x10000u) ? lane : (ent >> 8)) << 2), (int)ent);
         const bool live = g + lane < total;
         lds[live ? outr_off + (o & omask) : sink_off] = (uint8_t)ent;
+#if CD_WIDE
+        cd_fence();
+        {
+            const uint32_t done = g + CD_LANES <= total ? gb + CD_LANES : O + total;
+            if (done - F >= unit) {
+                /* one unit: unit / 16 lanes, 16 bytes each */
+                const uint32_t x = F + 16u * lane;
+                if (16u * lane < unit) {
+                    uint4 v;
+                    __builtin_memcpy(&v, lds + outr_off + (x & omask), 16);
+                    __builtin_memcpy(dst + x, &v, 16);
+                }
+                F += unit;
+            }
+        }
+#else
         if (g + CD_LANES <= total) dst[o] = (uint8_t)ent;
         else if (live) dst[o] = (uint8_t)ent;
         cd_fence();
+#endif
 #if CD_PIPEG
         tI = tIn;
 #endif
@@ -456,6 +508,7 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
 
     mark[lane] = 0u;            /* group tags are >= 1 */
     uint32_t loaded = 0, base = 0, O = 0;
+    uint32_t F = 0;             /* output [0, F) stored (CD_WIDE) */
     int32_t err = 0;
     bool first = true;
     while (first || base < in_len) {                     /* src/lzf_d.c:64, 146 */
@@ -469,10 +522,13 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
             break;
         }
         cd_output<CD_IN_RING1>(smem, CD_IN_RING1, omask, mark, (uint32_t)(tokpos - smem), dst, O, r.total,
-                               x < CD_ROUND, O + r.rel, r.tinfo, lane);
+                               x < CD_ROUND, O + r.rel, r.tinfo, lane, F);
         O += r.total;
         base = nbase;
     }
+#if CD_WIDE
+    cd_flush(smem, CD_IN_RING1, omask, dst, F, O, lane);   /* the rounds before a failing one, as the reference */
+#endif
     if (lane == 0) {
         bt.out_len[v] = err ? 0u : O;
         bt.err[v] = err;
@@ -559,7 +615,7 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
         }
     } else {
         uint8_t *dst = bt.out + bt.out_off[v];
-        uint32_t O = 0;
+        uint32_t O = 0, F = 0;  /* output [0, F) stored (CD_WIDE) */
         int32_t err = 0;
         mark[lane] = 0u;        /* group tags are >= 1 */
         cd_barrier();
@@ -572,11 +628,15 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
             if (err) break;      /* the failing round writes nothing */
             const uint32_t w = s.tok[lane];
             cd_output<CD_IN_RINGP>(smem, (uint32_t)(outr - smem), omask, mark, (uint32_t)(sink - smem), dst, O,
-                                   total, lane < ntok, O + (w & 0xFFFFu), (w >> 17) | ((w & 0x10000u) << 15), lane);
+                                   total, lane < ntok, O + (w & 0xFFFFu), (w >> 17) | ((w & 0x10000u) << 15), lane,
+                                   F);
             O += total;
             if (last) break;
             cd_barrier(tw);
         }
+#if CD_WIDE
+        cd_flush(smem, (uint32_t)(outr - smem), omask, dst, F, O, lane);   /* also before a failing round */
+#endif
 #ifdef CD_TIMING
         tw[0] += __builtin_amdgcn_s_memtime() - tw[2];
 #endif

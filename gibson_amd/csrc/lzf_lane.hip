@@ -931,6 +931,9 @@ extern "C" int lzf_gpu_debug_sites(unsigned long long *out16, int reset)
 #ifndef K2_NRES
 #define K2_NRES 1u
 #endif
+#ifndef K2_NOSTORE
+#define K2_NOSTORE 0        /* diagnostic: 1 = the output's 16-byte stores are skipped (timing only) */
+#endif
 #ifndef K2_LITMIN
 #define K2_LITMIN   8u       /* lanes of the wave that must take a free-literal trip for it to run */
 #endif
@@ -1006,7 +1009,8 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
             __builtin_memcpy(da + 12u, &l_, 4);                                    \
         } else {                                                                   \
             const uint4 v_ = make_uint4(pb0, pb1, pb2, (w_));                      \
-            __builtin_memcpy(da + 4u * fs, &v_, 16);                               \
+            if (!K2_NOSTORE || bt.max_len == 0xFFFFFFFFu)                          \
+                __builtin_memcpy(da + 4u * fs, &v_, 16);                           \
         }                                                                          \
         K2_SITE(8);                                                                \
     } while (0)
