@@ -383,7 +383,7 @@ __global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt,
 #define K3_THREADS 256u
 #endif
 #ifndef K3_CB
-#define K3_CB      16u          /* records per parse block: 64 bytes of one line (8: 32 bytes) */
+#define K3_CB      16u          /* records per parse block: 64 bytes of one line (8: 32 bytes, 32: the whole line) */
 #endif
 #ifndef K3_NRES
 #define K3_NRES    2u           /* candidate tests per loop iteration (2: 206.2 vs 210.8 ms for 1 + a memory-free one) */
@@ -515,8 +515,35 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
     uint4 W = make_uint4(0, 0, 0, 0);
 
     uint32_t o = 1u, run = 0u, p = 0u; /* o, run: the reference's op and lit (src/lzf_c.c:113-143) */
-    uint32_t cb = 0xFFFFFFF0u;         /* records [cb, cb + 16) in C0..C3 */
+    uint32_t cb = 0xFFFFFFE0u;         /* records [cb, cb + K3_CB) in C0..C3 (C4..C7) */
     uint4 C0 = W, C1 = W, C2 = W, C3 = W;
+#if K3_CB == 32
+    uint4 C4 = W, C5 = W, C6 = W, C7 = W;
+#endif
+    /* record d of the block: a select tree over the block's words (a dynamic
+     * index would put the block in scratch memory) */
+    const auto pick = [&](uint32_t d) -> uint32_t {
+        const bool b0 = d & 1u, b1 = d & 2u;
+        const uint32_t c0 = b1 ? (b0 ? C0.w : C0.z) : (b0 ? C0.y : C0.x);
+        const uint32_t c1 = b1 ? (b0 ? C1.w : C1.z) : (b0 ? C1.y : C1.x);
+#if K3_CB >= 16
+        const uint32_t c2 = b1 ? (b0 ? C2.w : C2.z) : (b0 ? C2.y : C2.x);
+        const uint32_t c3 = b1 ? (b0 ? C3.w : C3.z) : (b0 ? C3.y : C3.x);
+        const uint32_t lo = (d & 8u) ? ((d & 4u) ? c3 : c2) : ((d & 4u) ? c1 : c0);
+#if K3_CB == 32
+        const uint32_t c4 = b1 ? (b0 ? C4.w : C4.z) : (b0 ? C4.y : C4.x);
+        const uint32_t c5 = b1 ? (b0 ? C5.w : C5.z) : (b0 ? C5.y : C5.x);
+        const uint32_t c6 = b1 ? (b0 ? C6.w : C6.z) : (b0 ? C6.y : C6.x);
+        const uint32_t c7 = b1 ? (b0 ? C7.w : C7.z) : (b0 ? C7.y : C7.x);
+        const uint32_t hi = (d & 8u) ? ((d & 4u) ? c7 : c6) : ((d & 4u) ? c5 : c4);
+        return (d & 16u) ? hi : lo;
+#else
+        return lo;
+#endif
+#else
+        return (d & 4u) ? c1 : c0;
+#endif
+    };
     uint32_t cw = 0u, curw = 0u;       /* inserted-bitmap word of p, in flight */
     __shared__ uint32_t k3_ring[K3_RW][K3_THREADS];
     uint32_t *const ring = &k3_ring[0][threadIdx.x];
@@ -641,23 +668,18 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
                     C0 = cp[0];
 #endif
                     C1 = cp[1];
-#if K3_CB == 16
+#if K3_CB >= 16
                     C2 = cp[2];
                     C3 = cp[3];
 #endif
-                }
-                /* a select tree over the block's words (a dynamic index would
-                 * put the block in scratch memory) */
-                const bool b0 = d & 1u, b1 = d & 2u;
-                const uint32_t c0 = b1 ? (b0 ? C0.w : C0.z) : (b0 ? C0.y : C0.x);
-                const uint32_t c1 = b1 ? (b0 ? C1.w : C1.z) : (b0 ? C1.y : C1.x);
-#if K3_CB == 16
-                const uint32_t c2 = b1 ? (b0 ? C2.w : C2.z) : (b0 ? C2.y : C2.x);
-                const uint32_t c3 = b1 ? (b0 ? C3.w : C3.z) : (b0 ? C3.y : C3.x);
-                const uint32_t c = (d & 8u) ? ((d & 4u) ? c3 : c2) : ((d & 4u) ? c1 : c0);
-#else
-                const uint32_t c = (d & 4u) ? c1 : c0;
+#if K3_CB == 32
+                    C4 = cp[4];
+                    C5 = cp[5];
+                    C6 = cp[6];
+                    C7 = cp[7];
 #endif
+                }
+                const uint32_t c = pick(d);
                 rel = (c >> 13) & 7u;
                 q = p - 1u - (c & 0x1FFFu);
                 reln = c >> 29;
@@ -768,12 +790,7 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
                         const uint32_t d_ = p - cb, x_ = p - wb;
                         go = go && p < n - 2u && d_ < K3_CB && x_ < 16u && o < cap;
                         if (go) {
-                            const bool b0_ = d_ & 1u, b1_ = d_ & 2u;
-                            const uint32_t c0_ = b1_ ? (b0_ ? C0.w : C0.z) : (b0_ ? C0.y : C0.x);
-                            const uint32_t c1_ = b1_ ? (b0_ ? C1.w : C1.z) : (b0_ ? C1.y : C1.x);
-                            const uint32_t c2_ = b1_ ? (b0_ ? C2.w : C2.z) : (b0_ ? C2.y : C2.x);
-                            const uint32_t c3_ = b1_ ? (b0_ ? C3.w : C3.z) : (b0_ ? C3.y : C3.x);
-                            const uint32_t c_ = (d_ & 8u) ? ((d_ & 4u) ? c3_ : c2_) : ((d_ & 4u) ? c1_ : c0_);
+                            const uint32_t c_ = pick(d_);
                             go = (c_ & 0xE000u) == 0u;
                         }
                         /* a trip the wave takes only when enough lanes gain
@@ -930,7 +947,10 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
 
 /* records per value: a multiple of 16 (64 bytes) plus one block of slack, so
  * the parse's 64-byte blocks never straddle a line and never leave the value */
-static uint64_t rec_stride(uint32_t max_len) { return (((uint64_t)max_len + 15u) & ~15ull) + 16u; }
+static uint64_t rec_stride(uint32_t max_len)
+{
+    return (((uint64_t)max_len + K3_CB - 1u) & ~(uint64_t)(K3_CB - 1u)) + (K3_CB < 16u ? 16u : K3_CB);
+}
 static uint64_t rec_bstride(uint32_t max_len) { return ((((uint64_t)max_len + 31u) >> 5) + 3u) & ~3ull; }
 
 size_t lzf_table_scratch_per_value(uint32_t max_len)
