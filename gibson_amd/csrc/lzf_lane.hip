@@ -937,6 +937,12 @@ extern "C" int lzf_gpu_debug_sites(unsigned long long *out16, int reset)
 #ifndef K2_LITMIN
 #define K2_LITMIN   8u       /* lanes of the wave that must take a free-literal trip for it to run */
 #endif
+#ifndef K2_LITPRE
+#define K2_LITPRE   K2_LITMIN   /* lanes of the wave that must be at a literal for the path to run */
+#endif
+#ifndef K2_LITUNG
+#define K2_LITUNG   0u       /* trips taken without the per-trip gate */
+#endif
 #ifndef K2_LITX
 #define K2_LITX 3u       /* free literals taken after a literal in the same iteration (0: none) */
 #endif
@@ -1166,7 +1172,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                      * all (one ballot of the branch's lanes): on text, where
                      * few are, the wave skips the path */
                     bool go = true;
-                    if ((uint32_t)__builtin_popcountll(__ballot(true)) >= K2_LITMIN)
+                    if ((uint32_t)__builtin_popcountll(__ballot(true)) >= K2_LITPRE)
 #pragma unroll
                     for (uint32_t e_ = 0; e_ < K2_LITX; e_++) {
                         const uint32_t d_ = p - cb, x_ = p - wb;
@@ -1179,7 +1185,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                         /* a trip the wave takes only when enough lanes gain
                          * from it: on text, where few do, the others would
                          * wait through it */
-                        if ((uint32_t)__builtin_popcountll(__ballot(go)) < K2_LITMIN) break;
+                        if (e_ >= K2_LITUNG && (uint32_t)__builtin_popcountll(__ballot(go)) < K2_LITMIN) break;
                         if (go) {
                             K2_SITE(9);
                             curw |= 1u << (p & 31u);
