@@ -49,9 +49,10 @@ enum KernelGen { GEN_TABLE = 0, GEN_LANE = 1, GEN_WINDOW = 2, GEN_SERIAL = 3, GE
 constexpr uint32_t LANE_DEFAULT_MAX = 16384u;
 
 /* LZF_GPU_KERNEL picks the kernel generation, read per launch so one process
- * can A/B them.  Unset: the measured routing of launch_compress (the table
- * generation, lzf_cand.hip, for values of 4-64 KiB; the lane small class,
- * lzf_lane.hip, up to 4 KiB; window64 past 64 KiB and for small batches).
+ * can A/B them.  Unset: the measured routing of launch_compress (the lane
+ * generation -- the stream cand kernel, lzf_stream.hip, and the lane parse,
+ * lzf_lane.hip -- up to 16 KiB; the table generation, lzf_cand.hip, for values
+ * of 16-64 KiB; window64 past 64 KiB and for small batches).
  * "lane": the lane generation wherever it applies; "window": one wave per
  * value (window64 / tokpar64); "serial" (diagnostic build): the single-lane
  * first generation.  All are bit-exact; the GPU tests cross-check them. */
