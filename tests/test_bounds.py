@@ -87,6 +87,27 @@ def test_compress_writes_nothing_past_out_cap(oracle, nmax):
         assert (bytes(out[o:o + ln]) if ln else None) == exp
 
 
+@pytest.mark.parametrize("nmax", [4096, 16384, 65536])
+def test_free_literal_runs_at_tight_caps(oracle, nmax):
+    # whole waves of random and mixed-entropy values, so the parses'
+    # free-literal path (at least 8 lanes of a wave at a
+    # literal with no candidate) runs, and caps that run out inside such runs
+    rnd = random.Random(100 + nmax)
+    vals, caps = [], []
+    for i in range(320):
+        n = rnd.choice([nmax, rnd.randint(nmax // 2, nmax)])
+        kind = 4 if i % 3 else 3                       # random bytes, mixed entropy
+        v = synth(kind, 0x5EED0B30, i, n)
+        full = oracle.compress(v, n + n // 16 + 64)
+        F = len(full) if full else n
+        caps.append(max(1, rnd.choice([n - 4, F - 1, F, F + 33, rnd.randint(1, n), n // 3])))
+        vals.append(v)
+    out, offs, olen = _run_compress(vals, caps, nmax)
+    assert _guards_intact(out, offs, caps)
+    for v, c, o, ln in zip(vals, caps, offs, olen):
+        assert (bytes(out[o:o + ln]) if ln else None) == oracle.compress(v, c)
+
+
 def test_compress_refuses_value_past_stated_max_len(oracle):
     rnd = random.Random(3)
     vals = [synth(rnd.randrange(4), 0x5EED0B10, i, rnd.choice([900, 5000, 9000, 30000])) for i in range(200)]
