@@ -40,7 +40,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 import gibson_amd  # noqa: E402
-from gibson_amd.shard import reduce_stats, shard  # noqa: E402
+from gibson_amd.shard import reduce_stats, shard, spread_stats  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CHUNK_BYTES = 16 << 30  # codec chunk of a batch past this many input bytes
@@ -185,6 +185,17 @@ def _traffic(workload, kernel, count):
         return None, None
 
 
+def _spread(world, steps, k_lo, k_hi, w_lo, w_hi):
+    """min / max over ranks of the per-step device time (HIP events around
+    the rank's launches) and of the timed wall region: the imbalance the
+    max-over-ranks `ms_per_step` hides"""
+    return {"ranks": world,
+            "kernel_ms_min": round(k_lo * 1e3, 3), "kernel_ms_max": round(k_hi * 1e3, 3),
+            "wall_ms_per_step_min": round(w_lo / steps * 1e3, 3),
+            "wall_ms_per_step_max": round(w_hi / steps * 1e3, 3),
+            "kernel_imbalance": round(k_hi / k_lo, 4) if k_lo > 0 else None}
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -316,6 +327,7 @@ def main():
     c0 = (nch - 1) * chunk
     good = verify(c0, count - c0) and good
 
+    (k_lo, w_lo), (k_hi, w_hi) = spread_stats([t_comp + t_dec, wall], device=RED_DEV)
     (wall, t_comp, t_dec), (in_bytes_all, n_ok_all, c_bytes_all, bad_ranks) = reduce_stats(
         [wall, t_comp, t_dec], [count * n, n_ok, c_bytes, 0 if good else 1], device=RED_DEV)
 
@@ -359,6 +371,7 @@ def main():
                 "chunks": nch,
                 "chunk_values": chunk,
             },
+            "rank_spread": _spread(world, a.steps, k_lo, k_hi, w_lo, w_hi),
             "roofline": {
                 "bound": "hbm",
                 "kernel": dom,
@@ -453,6 +466,7 @@ def main_decompress(a, world, rank, dev, cfg_idx, kind, seed, n, count):
         good = good and not bool((diff & ok[c0:c0 + m]).any())
     del src
 
+    (k_lo, w_lo), (k_hi, w_hi) = spread_stats([t_dec, wall], device=RED_DEV)
     (wall, t_dec), (n_ok_all, c_bytes_all, bad_ranks) = reduce_stats(
         [wall, t_dec], [n_ok, c_bytes, 0 if good else 1], device=RED_DEV)
     if rank == 0:
@@ -487,6 +501,7 @@ def main_decompress(a, world, rank, dev, cfg_idx, kind, seed, n, count):
                 "kernels": gibson_amd.kernel_info(),
                 "roundtrip_ok": bad_ranks == 0,
             },
+            "rank_spread": _spread(world, a.steps, k_lo, k_hi, w_lo, w_hi),
             "roofline": {
                 "bound": "hbm",
                 "kernel": "lzf_decompress",

@@ -34,7 +34,7 @@ hipError_t lzf_launch_compress_serial(const LzfBatch &b, hipStream_t s);
 hipError_t lzf_launch_decompress_serial(const LzfBatch &b, hipStream_t s);
 #endif
 
-int lzf_lds_order_check(void);      /* lzf_selfcheck.hip */
+int lzf_lds_order_check(int dev);   /* lzf_selfcheck.hip */
 
 namespace {
 
@@ -53,18 +53,21 @@ constexpr uint32_t LANE_DEFAULT_MAX = 16384u;
  * generation -- the stream cand kernel, lzf_stream.hip, and the lane parse,
  * lzf_lane.hip -- up to 16 KiB; the table generation, lzf_cand.hip, for values
  * of 16-64 KiB; window64 past 64 KiB and for small batches).
- * "lane": the lane generation wherever it applies; "window": one wave per
- * value (window64 / tokpar64); "serial" (diagnostic build): the single-lane
- * first generation.  All are bit-exact; the GPU tests cross-check them. */
+ * "lane": the lane generation wherever it applies; "table": the table
+ * generation at any size it takes; "window": one wave per value (window64 /
+ * tokpar64).  Diagnostic build only: "serial" (the single-lane first
+ * generation) and "wtab" (the window-parse generation, lzf_wparse.hip, a
+ * measured prototype that is not routed).  All are bit-exact; the GPU tests
+ * cross-check them. */
 KernelGen kernel_gen()
 {
     const char *e = getenv("LZF_GPU_KERNEL");
 #ifdef LZF_DIAG
     if (e && !strcmp(e, "serial")) return GEN_SERIAL;
+    if (e && !strcmp(e, "wtab")) return GEN_WTAB;
 #endif
     if (e && !strcmp(e, "window")) return GEN_WINDOW;
     if (e && !strcmp(e, "lane")) return GEN_LANE;
-    if (e && !strcmp(e, "wtab")) return GEN_WTAB;
     if (e && !strcmp(e, "table")) return GEN_TABLE_ONLY;
     return GEN_TABLE;
 }
@@ -85,10 +88,16 @@ bool device_ok(int dev)
 
 /* The table, lane and window generations need the LDS to run a wave's
  * same-address ds_mskor_rtn_b32 in lane order (lzf_selfcheck.hip).  Checked
- * once per device before their first launch; where it does not hold, compress
- * batches go to window64.  LZF_GPU_FORCE_ORDER_FAIL=1 makes the check report
- * a violation (tests of the fallback). */
-int g_order[64];                     /* 0 unchecked, 1 held, -1 violated, -2 probe failed */
+ * per device before their first launch (on the probe's own stream, so the
+ * caller's stream and the rest of the device are not synchronised); where it
+ * does not hold, compress batches go to window64.  Only a definite answer is
+ * kept: a probe that could not run (an allocation or launch failure under
+ * load) routes this batch to window64 and is tried again on the next one.
+ * LZF_GPU_FORCE_ORDER_FAIL=1 makes the check report a violation (tests of
+ * the fallback).  A caller that captures compress launches in a HIP graph
+ * runs lzf_gpu_selfcheck() first, outside the capture. */
+int g_order[64];                     /* 0 unchecked, 1 held, -1 violated */
+int g_order_last[64];                /* the last probe's outcome, -2: it could not run */
 std::mutex g_order_mu;
 
 int lds_order_state(bool run)
@@ -98,10 +107,12 @@ int lds_order_state(bool run)
     std::lock_guard<std::mutex> lk(g_order_mu);
     if (!g_order[dev] && run) {
         const char *f = getenv("LZF_GPU_FORCE_ORDER_FAIL");
-        const int bad = (f && *f == '1') ? 1 : lzf_lds_order_check();
-        g_order[dev] = bad == 0 ? 1 : bad > 0 ? -1 : -2;
+        const int bad = (f && *f == '1') ? 1 : lzf_lds_order_check(dev);
+        g_order_last[dev] = bad == 0 ? 1 : bad > 0 ? -1 : -2;
+        if (bad >= 0) g_order[dev] = g_order_last[dev];
+        return g_order_last[dev];
     }
-    return g_order[dev];
+    return g_order[dev] ? g_order[dev] : g_order_last[dev];
 }
 
 bool lds_order_ok() { return lds_order_state(true) == 1; }
@@ -164,7 +175,8 @@ void scratch_free(Scratch &S)
 }
 
 enum ScratchUser { SU_LANE = 0, SU_TABLE = 1, SU_WTAB = 2 };
-uint32_t g_last_chunks = 0;          /* chunks of the last scratch-bound compress launch */
+/* chunks of this thread's last scratch-bound compress launch (kernel_info) */
+thread_local uint32_t g_last_chunks = 0;
 
 hipError_t lane_compress(const LzfBatch &b, hipStream_t s, ScratchUser who)
 {
@@ -174,13 +186,21 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s, ScratchUser who)
     if (e != hipSuccess) return e;
     Scratch &S = g_scratch[dev & 63];
     std::lock_guard<std::mutex> lk(S.mu);
+#ifdef LZF_DIAG
     const size_t per = who == SU_WTAB ? lzf_wtab_scratch_per_value(b.max_len)
                        : table        ? lzf_table_scratch_per_value(b.max_len)
                                       : lzf_lane_scratch_per_value(b.max_len);
+#else
+    const size_t per = table ? lzf_table_scratch_per_value(b.max_len) : lzf_lane_scratch_per_value(b.max_len);
+#endif
     size_t want = per * (size_t)b.count + 512;
     const size_t lim = scratch_limit(S.cap);
     if (want > lim) want = lim;
     if (want < 2 * per + 1024) want = 2 * per + 1024;     /* two pipeline halves */
+    /* an explicit cap binds even when an earlier batch grew the scratch past
+     * it: the buffer is given back and re-made at the cap */
+    const bool capped = getenv("LZF_GPU_SCRATCH_MB") != nullptr;
+    if (capped && S.cap > want && S.cap > lim) scratch_free(S);
     if (S.cap < want) {
         scratch_free(S);
         /* short of device memory: a smaller scratch only means more chunks */
@@ -197,11 +217,18 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s, ScratchUser who)
     }
     if (!S.ev && (e = hipEventCreateWithFlags(&S.ev, hipEventDisableTiming)) != hipSuccess) return e;
     if (S.used && S.last != s && (e = hipStreamWaitEvent(s, S.ev, 0)) != hipSuccess) return e;
-    if (who == SU_WTAB) {
-        e = lzf_launch_compress_wtab(b, s, S.p, S.cap, &g_last_chunks);
-    } else if (table) {
-        e = lzf_launch_compress_table(b, s, S.p, S.cap, &g_last_chunks);
-    } else {
+    /* the chunk size comes from the usable scratch: the buffer, or the cap
+     * when one is set below it */
+    const size_t use = capped && lim < S.cap ? (lim > 2 * per + 1024 ? lim : 2 * per + 1024) : S.cap;
+    if (table) {
+        e = lzf_launch_compress_table(b, s, S.p, use, &g_last_chunks);
+    }
+#ifdef LZF_DIAG
+    else if (who == SU_WTAB) {
+        e = lzf_launch_compress_wtab(b, s, S.p, use, &g_last_chunks);
+    }
+#endif
+    else {
 #ifdef LZF_DIAG
         const char *ff = getenv("LZF_GPU_LANE_FORCE_FIX");
         /* LZF_GPU_LANE_PIPE=1 overlaps the two kernels of consecutive chunks
@@ -213,10 +240,10 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s, ScratchUser who)
             for (int k = 0; k < 4; k++)
                 if ((e = hipEventCreateWithFlags(&S.pev[k], hipEventDisableTiming)) != hipSuccess) return e;
         }
-        e = lzf_launch_compress_lane(b, s, S.p, S.cap, (ff && *ff == '1') ? 1u : 0u, pipe ? S.aux : nullptr,
+        e = lzf_launch_compress_lane(b, s, S.p, use, (ff && *ff == '1') ? 1u : 0u, pipe ? S.aux : nullptr,
                                      pipe ? S.pev : nullptr, &g_last_chunks);
 #else
-        e = lzf_launch_compress_lane(b, s, S.p, S.cap, 0u, nullptr, nullptr, &g_last_chunks);
+        e = lzf_launch_compress_lane(b, s, S.p, use, 0u, nullptr, nullptr, &g_last_chunks);
 #endif
     }
     if (e != hipSuccess) return e;
@@ -257,8 +284,10 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
         return (lzf_lane_compress_supported(b.max_len) && b.count >= lane_min_count(b.max_len))
                    ? lane_compress(b, s, SU_LANE)
                    : lzf_launch_compress(b, s);
+#ifdef LZF_DIAG
     case GEN_WTAB:
         return lzf_wtab_compress_supported(b.max_len) ? lane_compress(b, s, SU_WTAB) : lzf_launch_compress(b, s);
+#endif
     case GEN_TABLE_ONLY:
         return (lzf_table_compress_supported(b.max_len) && b.count >= lane_min_count(b.max_len))
                    ? lane_compress(b, s, SU_TABLE)
@@ -273,14 +302,17 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
          * table generation (two-link records, lzf_cand.hip) */
         if (b.count < lane_min_count(b.max_len) || !lzf_table_compress_supported(b.max_len))
             return lzf_launch_compress(b, s);
-        return lane_compress(b, s, b.max_len > LANE_DEFAULT_MAX ? SU_TABLE : SU_LANE);
+        /* the lane generation where its kernel 1 takes the batch (a
+         * diagnostic LZF_GPU_CAND=small stops at 4 KiB), else the table one */
+        return lane_compress(b, s, b.max_len <= LANE_DEFAULT_MAX && lzf_lane_compress_supported(b.max_len)
+                                       ? SU_LANE : SU_TABLE);
     }
 }
 
-/* The lane decoder (one lane per stream) is bit-exact but, streaming 64
- * values per wave through L2, slower than tokpar64 on the BASELINE shapes
- * (DESIGN.md §4.3); the lane generation therefore decodes with tokpar64
- * unless LZF_GPU_DECOMPRESS=lane asks for the lane decoder. */
+/* The lane decoder (one lane per stream, diagnostic build) is bit-exact but,
+ * streaming 64 values per wave through L2, slower than pipe / tokpar64 on
+ * the BASELINE shapes; it runs only when
+ * LZF_GPU_DECOMPRESS=lane asks for it. */
 bool lane_decoder()
 {
 #ifdef LZF_DIAG
@@ -895,7 +927,9 @@ int lzf_gpu_lds_order_probe(void)
 {
     int rc = current_device_ok();
     if (rc) return rc;
-    return lzf_lds_order_check();
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return LZF_GPU_ENODEV;
+    return lzf_lds_order_check(dev);
 }
 
 const char *lzf_gpu_kernel_info(void)
@@ -909,10 +943,12 @@ const char *lzf_gpu_kernel_info(void)
         s = std::string("compress=") + lzf_compress_kernel_name() + " decompress=" +
             lzf_decompress_kernel_name();
         break;
+#ifdef LZF_DIAG
     case GEN_WTAB:
         s = std::string("compress=wtab(cand_q1+wparse; window64 past 64 KiB) decompress=") +
             lzf_decompress_kernel_name();
         break;
+#endif
     case GEN_TABLE_ONLY:
         s = std::string("compress=table(cand_table+parse_rec; window64 past 64 KiB or below ") +
             std::to_string(lane_min_count(4096u)) + " values of <= 4 KiB / " +
@@ -942,7 +978,7 @@ const char *lzf_gpu_kernel_info(void)
     {
         const int st = lds_order_state(false);
         s += std::string(" lds_order=") + (st == 1 ? "held" : st == -1 ? "violated(compress->window64)"
-                                           : st == -2 ? "probe-failed(compress->window64)" : "unchecked");
+                                           : st == -2 ? "probe-failed(retried)" : "unchecked");
         if (g_last_chunks) s += " scratch_chunks=" + std::to_string(g_last_chunks);
     }
     return s.c_str();

@@ -974,11 +974,15 @@ hipError_t lzf_launch_compress_table(const LzfBatch &b, hipStream_t s, void *scr
     /* diagnostics: LZF_GPU_TABLE_STAGE=1 runs kernel 1 only (its own time) */
     const char *stg = getenv("LZF_GPU_TABLE_STAGE");
     const bool cand_only = stg && *stg == '1';
-    /* kernel 1: the per-value pipeline (lzf_cand_table_kernel) or the stream
-     * form (lzf_stream.hip: values back to back, no per-value table clear
-     * or pipeline drain); LZF_GPU_TCAND=table|stream */
+    /* kernel 1: the per-value pipeline (lzf_cand_table_kernel); in the
+     * diagnostic build LZF_GPU_TCAND=stream takes the stream kernel's record
+     * form instead (lzf_stream.hip, bit-exact, slower: DESIGN.md §4.6) */
+#ifdef LZF_DIAG
     const char *tc = getenv("LZF_GPU_TCAND");
     const bool stream = tc && !strcmp(tc, "stream");
+#else
+    constexpr bool stream = false;
+#endif
     LzfRecScratch sc;
     sc.rec = (uint32_t *)scratch;
     sc.bits = (uint32_t *)((uint8_t *)scratch + ((chunk * rstride * 4u + 255u) & ~255ull));
@@ -1002,7 +1006,9 @@ hipError_t lzf_launch_compress_table(const LzfBatch &b, hipStream_t s, void *scr
         /* one 512-thread workgroup per CU (the table is 128 KiB), persistent */
         const uint32_t g = cnt < (uint32_t)cus ? cnt : (uint32_t)cus;
         if (stream) {
+#ifdef LZF_DIAG
             if ((e = lzf_launch_cand_stream_rec(c, sc, s)) != hipSuccess) return e;
+#endif
         } else {
             hipLaunchKernelGGL(lzf_cand_table_kernel, dim3(g), dim3(KT_THREADS), 0, s, c, sc);
             if ((e = hipGetLastError()) != hipSuccess) return e;

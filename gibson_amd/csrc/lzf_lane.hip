@@ -1640,14 +1640,18 @@ static bool lane_ring_enabled()
 
 /* kernel 1 of the lane generation: the stream form (lzf_stream.hip: the
  * exact table, values back to back in one pipeline per CU; any value of at
- * most 64 KiB), or -- LZF_GPU_CAND=small, read per launch, a cross-check --
- * the small class (values of at most 4 KiB; the diagnostic build's ring and
+ * most 64 KiB), or -- diagnostic build, LZF_GPU_CAND=small, read per launch,
+ * a cross-check -- the small class (values of at most 4 KiB; the ring and
  * mid classes past that).  json4k 1 M x 4 KiB: 45.9 ms with the stream form,
  * 48.7 with the small class (cand 17.3 vs 19.9 ms, rocprof). */
 static bool lane_cand_small()
 {
+#ifdef LZF_DIAG
     const char *e = getenv("LZF_GPU_CAND");
     return e && !strcmp(e, "small");
+#else
+    return false;
+#endif
 }
 
 const char *lzf_lane_cand_name(void) { return lane_cand_small() ? "cand_small" : "cand_stream"; }
@@ -1656,8 +1660,8 @@ bool lzf_lane_compress_supported(uint32_t max_len)
 {
 #ifndef LZF_DIAG
     /* the stream form takes any value the parse's 13-bit offsets and 16-bit
-     * positions cover; the small class values of at most 4 KiB */
-    return lane_cand_small() ? max_len <= KS_MAXN : max_len <= LZF_SLOTS;
+     * positions cover */
+    return max_len <= LZF_SLOTS;
 #else
     if (!lane_cand_small()) return max_len <= LZF_SLOTS;
     if (max_len <= KS8_MAXN) return true;
@@ -1696,19 +1700,16 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
         sc[h].bstride = bstride;
         sc[h].force_fix = force_fix;
     }
-    /* the small-class kernel is persistent: as many one-wave workgroups as
-     * stay resident (LDS-bound), each walking the batch */
+    /* the small-class kernel (diagnostic) is persistent: as many one-wave
+     * workgroups as stay resident (LDS-bound), each walking the batch */
 #ifdef LZF_DIAG
     const bool ring = b.max_len > KS8_MAXN && b.max_len <= KR64_MAXN && lane_ring_enabled();
     const void *small_fn = b.max_len <= KS_MAXN    ? (const void *)lzf_cand_small_kernel<4u, KS_MAXN, KS_WIN>
                            : b.max_len <= KS8_MAXN ? (const void *)lzf_cand_small_kernel<3u, KS8_MAXN, KS8_WIN>
                            : b.max_len <= KR_MAXN  ? (const void *)lzf_cand_ring_kernel<KR_MAXN, KR_WIN>
                                                    : (const void *)lzf_cand_ring_kernel<KR64_MAXN, KR_WIN>;
-#else
-    const void *small_fn = (const void *)lzf_cand_small_kernel<4u, KS_MAXN, KS_WIN>;
-#endif
     uint32_t small_grid = 256u * 8u;
-    {
+    if (lane_cand_small()) {
         int dev = 0, cus = 0;
         hipFuncAttributes fa;
         if (hipGetDevice(&dev) == hipSuccess &&
@@ -1723,6 +1724,7 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
             small_grid = (uint32_t)cus * per;
         }
     }
+#endif
     /* kernel 2: one lane per value; LZF_GPU_LANE_PARSE=wave selects the wave
      * form for the small class (slower today) */
 #ifdef LZF_DIAG
@@ -1755,12 +1757,12 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
         if (pipe && i >= 2u && (e = hipStreamWaitEvent(s, ev[2 + h], 0)) != hipSuccess) return e;
         if (stream) {
             if ((e = lzf_launch_cand_stream(c, sc[h], s)) != hipSuccess) return e;
-        } else if (b.max_len <= KS_MAXN) {
-            const uint32_t g = cnt < small_grid ? cnt : small_grid;
-            hipLaunchKernelGGL((lzf_cand_small_kernel<4u, KS_MAXN, KS_WIN>), dim3(g), dim3(64), 0, s, c, sc[h]);
         }
 #ifdef LZF_DIAG
-        else if (b.max_len <= KS8_MAXN) {
+        else if (b.max_len <= KS_MAXN) {
+            const uint32_t g = cnt < small_grid ? cnt : small_grid;
+            hipLaunchKernelGGL((lzf_cand_small_kernel<4u, KS_MAXN, KS_WIN>), dim3(g), dim3(64), 0, s, c, sc[h]);
+        } else if (b.max_len <= KS8_MAXN) {
             const uint32_t g = cnt < small_grid ? cnt : small_grid;
             hipLaunchKernelGGL((lzf_cand_small_kernel<3u, KS8_MAXN, KS8_WIN>), dim3(g), dim3(64), 0, s, c, sc[h]);
         } else if (ring) {

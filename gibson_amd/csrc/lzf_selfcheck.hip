@@ -20,6 +20,8 @@
  * lane checks its returned half and its table word against the lane-order
  * image it computes itself, and counts mismatches.
  */
+#include <mutex>
+
 #include "lzf_internal.h"
 
 __device__ __forceinline__ uint32_t sc_half(uint32_t lane, uint32_t blk, uint32_t nhalf, uint32_t mode)
@@ -55,19 +57,37 @@ __global__ __launch_bounds__(64) void lzf_lds_order_probe_kernel(uint32_t *bad, 
 }
 
 /* mismatch count over all patterns (0: lane order held), or a negative
- * LZF_GPU_E* code; runs synchronously on the current device */
-int lzf_lds_order_check(void)
+ * LZF_GPU_E* code.  Runs on a non-blocking stream of its own with a counter
+ * and a pinned result word made once per device, so it neither waits for
+ * nor holds up the caller's streams (the device is not synchronised). */
+int lzf_lds_order_check(int dev)
 {
-    uint32_t *d = nullptr, h = 0;
-    if (hipMalloc(&d, sizeof(uint32_t)) != hipSuccess) return -4;
-    int rc = 0;
-    if (hipMemset(d, 0, sizeof(uint32_t)) != hipSuccess) rc = -2;
+    static std::mutex mu;
+    static hipStream_t st[64];
+    static uint32_t *cnt[64], *res[64];
+    if (dev < 0 || dev >= 64) return -2;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!st[dev] && hipStreamCreateWithFlags(&st[dev], hipStreamNonBlocking) != hipSuccess) {
+        st[dev] = nullptr;
+        return -2;
+    }
+    if (!cnt[dev] && hipMalloc(&cnt[dev], sizeof(uint32_t)) != hipSuccess) {
+        cnt[dev] = nullptr;
+        return -4;
+    }
+    if (!res[dev] && hipHostMalloc(&res[dev], sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+        res[dev] = nullptr;
+        return -4;
+    }
+    int rc = hipMemsetAsync(cnt[dev], 0, sizeof(uint32_t), st[dev]) == hipSuccess ? 0 : -2;
     for (uint32_t mode = 0; mode < 2u && !rc; mode++)
         for (uint32_t nh = 1; nh <= 128u && !rc; nh *= 2u) {
-            hipLaunchKernelGGL(lzf_lds_order_probe_kernel, dim3(1024), dim3(64), 0, 0, d, nh, mode);
+            hipLaunchKernelGGL(lzf_lds_order_probe_kernel, dim3(1024), dim3(64), 0, st[dev], cnt[dev], nh, mode);
             if (hipGetLastError() != hipSuccess) rc = -2;
         }
-    if (!rc && (hipMemcpy(&h, d, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)) rc = -2;
-    (void)hipFree(d);
-    return rc ? rc : (int)h;
+    if (!rc && hipMemcpyAsync(res[dev], cnt[dev], sizeof(uint32_t), hipMemcpyDeviceToHost, st[dev]) != hipSuccess)
+        rc = -2;
+    if (!rc && hipStreamSynchronize(st[dev]) != hipSuccess) rc = -2;
+    (void)hipGetLastError();
+    return rc ? rc : (int)*res[dev];
 }

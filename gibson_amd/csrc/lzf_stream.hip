@@ -519,9 +519,11 @@ hipError_t lzf_launch_cand_stream(const LzfBatch &b, const LzfLaneScratch &sc, h
     return hipGetLastError();
 }
 
+#ifdef LZF_DIAG   /* the record form: a cross-check of the table generation's kernel 1 */
 hipError_t lzf_launch_cand_stream_rec(const LzfBatch &b, const LzfRecScratch &sc, hipStream_t s)
 {
     hipLaunchKernelGGL(lzf_cand_stream_kernel<true>, dim3(ks_grid(b.count)), dim3(KS_THR), 0, s, b,
                        (uint8_t *)sc.rec, sc.rstride);
     return hipGetLastError();
 }
+#endif

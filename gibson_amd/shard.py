@@ -26,3 +26,14 @@ def reduce_stats(maxes, sums, device="cpu"):
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
         dist.all_reduce(ts, op=dist.ReduceOp.SUM)
     return tm.tolist(), ts.tolist()
+
+
+def spread_stats(values, device="cpu"):
+    """(min, max) over the process group of each of `values` (one per rank):
+    the per-rank imbalance bench.py reports beside the max it times by."""
+    t = torch.tensor([float(v) for v in values] + [-float(v) for v in values], dtype=torch.float64,
+                     device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    k = len(values)
+    return [-x for x in t[k:].tolist()], t[:k].tolist()

@@ -16,6 +16,8 @@ Files:
   corpus.json  randomized compress cases over kinds x sizes x out_len regimes
                (incl. the exact success/failure boundary), plus decoder cases
                (valid streams, truncations, corruptions, tight out_len)
+  config0.json BASELINE configs[0]: the 64 KiB text value at seed 0x5EED0001,
+               its reference stream (sha256, length) and round trip
   digests.json full-batch digests of the BASELINE configs' generators: the
                first 64 K values of configs[1..4] (and all 256 K of configs[2])
                compressed by the reference at out_len = n-4 (src/query.c:385);
@@ -162,9 +164,10 @@ DIGEST_CONFIGS = [
     (2, 2, 0x5EED0003, 65536, 262144),
     (3, 0, 0x5EED0004, 8192, 65536),
     (4, 3, 0x5EED0005, 16384, 65536),
-    # the production routes at their real batch sizes: >= 163 840 values of
-    # <= 4 KiB take the lane small class, >= 81 920 of <= 16 KiB the table
-    # generation (lzf_api.cpp lane_min_count)
+    # the production routes at their real batch sizes (at least
+    # lzf_api.cpp lane_min_count values: 163 840 of <= 4 KiB, 81 920 of
+    # <= 16 KiB): both take the lane generation, the stream cand kernel
+    # (lzf_stream.hip) and the lane parse
     (1, 1, 0x5EED0002, 4096, 262144),
     (4, 3, 0x5EED0005, 16384, 131072),
 ]
@@ -201,8 +204,32 @@ def digests():
     return res
 
 
+def config0():
+    """BASELINE configs[0]: one 64 KiB Zipf-text value (SYN_TEXT, seed
+    0x5EED0001, index 0) through the reference lzf_compress at out_len = n-4
+    (src/query.c:385) and back through lzf_decompress at the server's
+    out_len = maxrequestsize (4 MiB, src/default.h:45; src/net.c:1234)."""
+    n = 65536
+    data = synth(0, 0x5EED0001, 0, n)
+    stream = ref_compress(data, n - 4)
+    assert stream
+    r, e, out = ref_decompress(stream, 4 << 20)
+    assert r == n and e == 0 and out == data          # the reference's own round trip
+    return {"config": 0, "kind": 0, "seed": 0x5EED0001, "index": 0, "n": n,
+            "in_sha256": hashlib.sha256(data).hexdigest(), "out_len": n - 4,
+            "stream_len": len(stream), "stream_sha256": hashlib.sha256(stream).hexdigest(),
+            "decode_out_len": 4 << 20, "decode_result": r, "decode_errno": e}
+
+
 def main():
     here = os.path.dirname(os.path.abspath(__file__))
+    if len(sys.argv) > 1 and sys.argv[1] == "config0":
+        c0 = config0()
+        with open(os.path.join(here, "config0.json"), "w") as f:
+            json.dump({"generator": "tests/golden/make_golden.py config0",
+                       "source": "oracle/_ref/liblzf_ref.so (reference lzf_c.c, lzf_d.c)", **c0}, f, indent=1)
+        print("config0", c0["stream_len"], c0["stream_sha256"][:16])
+        return 0
     if len(sys.argv) > 1 and sys.argv[1] == "digests":
         with open(os.path.join(here, "digests.json"), "w") as f:
             json.dump({"generator": "tests/golden/make_golden.py digests",

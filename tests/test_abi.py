@@ -52,6 +52,36 @@ def test_no_cpu_codec_in_product_library():
     assert b"ref_lzf" not in data
 
 
+def _kernels(path):
+    # host-side stubs of the kernels a library can launch (nm of the .so)
+    import subprocess
+    out = subprocess.run(["nm", "-DC", "--defined-only", path], capture_output=True, text=True,
+                         check=True).stdout
+    return {m.group(1) for m in re.finditer(r"__device_stub__(?:void )?(\w+)", out)}
+
+
+# the kernels the product routing launches, and nothing else
+ROUTED = {"lzf_cand_stream_kernel", "lzf_parse_lane_kernel", "lzf_cand_table_kernel", "lzf_parse_rec_kernel",
+          "lzf_compress_window_kernel", "lzf_decompress_pipe_kernel", "lzf_decompress_tokpar_kernel",
+          "lzf_dsize_kernel", "lzf_lds_order_probe_kernel", "lzf_synth_kernel", "lzf_frame_size_kernel",
+          "lzf_frame_scan_kernel", "lzf_frame_write_kernel", "lzf_frame_check_kernel"}
+# cross-check forms: the diagnostic build only
+DIAG_ONLY = {"lzf_wparse_kernel", "lzf_cand_q1_kernel", "lzf_cand_small_kernel", "lzf_cand_ring_kernel",
+             "lzf_cand_mid_kernel", "lzf_compress_serial_kernel", "lzf_decompress_serial_kernel",
+             "lzf_decompress_lane_kernel", "lzf_parse_wave_kernel"}
+
+
+def test_product_library_holds_only_routed_kernels():
+    prod = _kernels(gibson_amd.lib_path())
+    assert prod == ROUTED, (sorted(prod - ROUTED), sorted(ROUTED - prod))
+    data = open(gibson_amd.lib_path(), "rb").read()
+    for name in ("lzf_launch_compress_wtab", "lzf_launch_cand_stream_rec", "lzf_launch_compress_serial"):
+        assert name.encode() not in data, name
+    diag = gibson_amd.lzf.diag_lib_path()
+    if os.path.exists(diag):
+        assert DIAG_ONLY <= _kernels(diag)
+
+
 def test_version_constant():
     assert gibson_amd.LZF_VERSION == 0x0105
 

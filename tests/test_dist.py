@@ -22,7 +22,7 @@ def _worker(rank, world, port, total, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from gibson_amd.shard import global_indices, reduce_stats
+    from gibson_amd.shard import global_indices, reduce_stats, spread_stats
     from tests.oracle_lib import Oracle, synth
     per = total // world
     idx = global_indices(rank, world, per)
@@ -34,7 +34,8 @@ def _worker(rank, world, port, total, q):
         in_bytes += len(v)
         comp += len(c) if c else 0
     (tmax,), (b, cb, nv) = reduce_stats([float(rank + 1)], [in_bytes, comp, len(idx)])
-    q.put((rank, idx, tmax, b, cb, nv, comp))
+    (lo, clo), (hi, chi) = spread_stats([10.0 * (rank + 1), comp])
+    q.put((rank, idx, tmax, b, cb, nv, comp, lo, hi, clo, chi))
     dist.destroy_process_group()
 
 
@@ -59,3 +60,6 @@ def test_round_robin_two_ranks():
         assert r[3] == total * 512                     # summed bytes
         assert r[5] == total
     assert res[0][4] == res[0][6] + res[1][6]          # summed compressed bytes
+    for r in res:                                      # per-rank spread: min / max over ranks
+        assert (r[7], r[8]) == (10.0, 20.0)
+        assert (r[9], r[10]) == (min(res[0][6], res[1][6]), max(res[0][6], res[1][6]))

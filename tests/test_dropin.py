@@ -106,6 +106,30 @@ def test_single_call_latency_recorded(oracle):
     assert all(u < 20000 for u in res.values())
 
 
+def _config0():
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "config0.json")) as f:
+        return json.load(f)
+
+
+def test_config0_roundtrip_dropin():
+    """BASELINE configs[0] by its own generator: the 64 KiB text value at seed
+    0x5EED0001 through the drop-in lzf_compress (out_len = n-4,
+    src/query.c:385) and lzf_decompress (out_len = maxrequestsize,
+    src/net.c:1234): the stream is the reference's (tests/golden/config0.json,
+    from oracle/_ref) and decodes to the value."""
+    import hashlib
+    import gibson_amd
+    c = _config0()
+    v = synth(c["kind"], c["seed"], c["index"], c["n"])
+    assert hashlib.sha256(v).hexdigest() == c["in_sha256"]
+    s = gibson_amd.lzf_compress(v, c["out_len"])
+    assert s is not None and len(s) == c["stream_len"]
+    assert hashlib.sha256(s).hexdigest() == c["stream_sha256"]
+    out, e = gibson_amd.lzf_decompress(s, c["decode_out_len"])
+    assert (len(out), e) == (c["decode_result"], c["decode_errno"]) and out == v
+
+
 def test_release_then_reuse(oracle):
     import gibson_amd
     from tests.gpu_batch import gpu_compress

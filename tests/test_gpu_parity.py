@@ -21,7 +21,8 @@ pytestmark = pytest.mark.gpu
 # "default": the library's routing (lane generation with the stream cand
 # kernel up to 16 KiB, table generation to 64 KiB); the rest forced
 GENERATIONS = ["default", "table", "table-stream", "wtab", "lane", "lane-small", "window", "serial", "lane-diag"]
-DIAG = {"serial", "lane-diag"}      # cross-check forms: the diagnostic build only
+# cross-check forms the product routing never takes: the diagnostic build only
+DIAG = {"serial", "lane-diag", "wtab", "table-stream", "lane-small"}
 GEN_ENV = {
     "default": {},
     "table": {"LZF_GPU_KERNEL": "table"},
@@ -304,42 +305,76 @@ def test_lane_ring_class(oracle, monkeypatch, align, diag):
     assert gpu_decompress(streams, [len(v) for v in origs]) == [(v, 0) for v in origs]
 
 
+def _chunks():
+    # scratch chunks of this thread's last scratch-bound compress launch
+    import re
+    import gibson_amd
+    m = re.search(r"scratch_chunks=(\d+)", gibson_amd.kernel_info())
+    return int(m.group(1)) if m else 0
+
+
+def _chunked_compress(oracle, vals, caps):
+    # the scratch is one per device, shared by every thread, and earlier tests
+    # grew it far past 1 MiB: the cap must still bind (the buffer is re-made
+    # at it), and the launch must really have run in several chunks
+    from tests.gpu_batch import gpu_compress
+    assert gpu_compress(vals, caps, align=3) == [oracle.compress(v, c) for v, c in zip(vals, caps)]
+    n = _chunks()
+    assert n > 1, f"scratch_chunks={n}"
+    return n
+
+
 @pytest.mark.parametrize("nmax", [4096, 8192, 16384, 65536])
 @pytest.mark.parametrize("cand", ["stream", "small"])
 def test_lane_scratch_chunks(oracle, monkeypatch, nmax, cand, diag):
-    # a small compress scratch cap runs the lane kernels over many chunks;
-    # the scratch is per host thread, so a fresh thread sees the cap
-    import threading
-    from tests.gpu_batch import gpu_compress
+    # a 1 MiB compress scratch cap runs the lane kernels over many chunks
     monkeypatch.setenv("LZF_GPU_KERNEL", "lane")
     monkeypatch.setenv("LZF_GPU_CAND", cand)
-    monkeypatch.setenv("LZF_GPU_SCRATCH_MB", "4")
+    monkeypatch.setenv("LZF_GPU_SCRATCH_MB", "1")
     rnd = random.Random(nmax)
     vals = [synth(rnd.randrange(6), 0x5EED00FA, i, rnd.randint(1, nmax)) for i in range(400)]
-    caps = [max(1, len(v) - 4) for v in vals]
-    out = {}
-    th = threading.Thread(target=lambda: out.setdefault("r", gpu_compress(vals, caps, align=3)))
-    th.start()
-    th.join()
-    assert out["r"] == [oracle.compress(v, c) for v, c in zip(vals, caps)]
+    _chunked_compress(oracle, vals, [max(1, len(v) - 4) for v in vals])
 
 
 @pytest.mark.parametrize("nmax", [4096, 65536])
-def test_table_scratch_chunks(oracle, monkeypatch, nmax):
-    # the table generation over many scratch chunks (4 MiB cap on a fresh
-    # host thread: the scratch is per host thread)
-    import threading
-    from tests.gpu_batch import gpu_compress
-    monkeypatch.setenv("LZF_GPU_KERNEL", "table")
-    monkeypatch.setenv("LZF_GPU_SCRATCH_MB", "4")
+@pytest.mark.parametrize("gen", ["table", "wtab"])
+def test_table_scratch_chunks(oracle, monkeypatch, nmax, gen):
+    # the table generation (and the window generation, diagnostic build)
+    # over many scratch chunks
+    monkeypatch.setenv("LZF_GPU_KERNEL", gen)
+    monkeypatch.setenv("LZF_GPU_SCRATCH_MB", "1")
     rnd = random.Random(nmax + 1)
     vals = [synth(rnd.randrange(6), 0x5EED00FB, i, rnd.randint(1, nmax)) for i in range(300)]
     caps = [max(1, len(v) - 4) for v in vals]
-    out = {}
-    th = threading.Thread(target=lambda: out.setdefault("r", gpu_compress(vals, caps, align=3)))
-    th.start()
-    th.join()
-    assert out["r"] == [oracle.compress(v, c) for v, c in zip(vals, caps)]
+    if gen == "wtab":
+        with _diag():
+            _chunked_compress(oracle, vals, caps)
+    else:
+        _chunked_compress(oracle, vals, caps)
+
+
+def test_scratch_chunks_default_route(oracle, monkeypatch):
+    # the product routing (lane generation, stream cand kernel) under a cap
+    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.setenv("LZF_GPU_SCRATCH_MB", "1")
+    rnd = random.Random(99)
+    vals = [synth(rnd.randrange(6), 0x5EED00FC, i, rnd.randint(1, 16384)) for i in range(300)]
+    _chunked_compress(oracle, vals, [max(1, len(v) - 4) for v in vals])
+
+
+@pytest.mark.parametrize("n", [8192, 16384])
+def test_default_route_with_small_cand_knob(oracle, monkeypatch, diag, n):
+    # LZF_GPU_CAND=small (diagnostic) takes values of at most 4 KiB: the
+    # default routing then sends 8 / 16 KiB batches to the table generation
+    # instead of failing the launch
+    monkeypatch.delenv("LZF_GPU_KERNEL", raising=False)
+    monkeypatch.setenv("LZF_GPU_CAND", "small")
+    monkeypatch.setenv("LZF_GPU_LANE_RING", "0")
+    rnd = random.Random(n)
+    vals = [synth(rnd.randrange(6), 0x5EED00FD, i, rnd.randint(n // 2, n)) for i in range(200)]
+    caps = [max(1, len(v) - 4) for v in vals]
+    from tests.gpu_batch import gpu_compress
+    assert gpu_compress(vals, caps) == [oracle.compress(v, c) for v, c in zip(vals, caps)]
 
 
 @pytest.mark.parametrize("align", [16, 3])
@@ -501,19 +536,34 @@ def test_full_batch_digest_and_roundtrip(kind, seed, n, count, digests, monkeypa
 @pytest.mark.parametrize("gen", ["table", "lane-small"])
 def test_full_batch_digest_other_cand(kind, seed, n, count, gen, digests, monkeypatch):
     # the production-size digests through the generations the routing no
-    # longer takes there: the table generation, and (4 KiB) the small class
+    # longer takes there: the table generation, and (4 KiB, diagnostic build)
+    # the small class
     if gen == "lane-small" and n > 4096:
         pytest.skip("the small class takes values of at most 4 KiB")
     monkeypatch.delenv("LZF_GPU_LANE_MIN", raising=False)
     for k, v in GEN_ENV[gen].items():
         monkeypatch.setenv(k, v)
-    _digest_case(kind, seed, n, count, digests)
+    if gen in DIAG:
+        with _diag():
+            _digest_case(kind, seed, n, count, digests)
+    else:
+        _digest_case(kind, seed, n, count, digests)
 
 
 @pytest.mark.parametrize("kind,seed,n,count", [c for c in CONFIGS if c[3] <= 65536])
-def test_full_batch_digest_wtab(kind, seed, n, count, digests, monkeypatch):
+def test_full_batch_digest_wtab(kind, seed, n, count, digests, monkeypatch, diag):
     monkeypatch.setenv("LZF_GPU_KERNEL", "wtab")
     _digest_case(kind, seed, n, count, digests)
+
+
+def test_full_batch_digest_chunked_scratch(digests, monkeypatch):
+    # configs[2]'s 262 144 x 64 KiB under a 16 GiB scratch cap: the table
+    # generation in five chunks (a GPU-sharing server's route), bit-exact by
+    # the reference's digest
+    monkeypatch.delenv("LZF_GPU_LANE_MIN", raising=False)
+    monkeypatch.setenv("LZF_GPU_SCRATCH_MB", "16384")
+    _digest_case(2, 0x5EED0003, 65536, 262144, digests)
+    assert _chunks() == 5, _chunks()
 
 
 def _digest_case(kind, seed, n, count, digests):

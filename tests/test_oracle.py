@@ -130,3 +130,20 @@ def test_oracle_matches_full_batch_digest():
     L.oracle_compress_batch(src.ctypes.data, offs.ctypes.data, ln.ctypes.data, count, out.ctypes.data,
                             offs.ctypes.data, cap.ctypes.data, olen.ctypes.data, 1)
     assert batch_digest(out, n, olen) == d["sha256"]
+
+
+def test_oracle_config0_fixture(oracle):
+    # BASELINE configs[0] (tests/golden/config0.json, from the reference):
+    # the oracle's stream and round trip for the 64 KiB text value at seed
+    # 0x5EED0001, out_len n-4 (src/query.c:385), decode at 4 MiB
+    import hashlib
+    import json
+    import os
+    with open(os.path.join(oracle_lib.ROOT, "tests", "golden", "config0.json")) as f:
+        c = json.load(f)
+    v = synth(c["kind"], c["seed"], c["index"], c["n"])
+    assert hashlib.sha256(v).hexdigest() == c["in_sha256"]
+    s = oracle.compress(v, c["out_len"])
+    assert len(s) == c["stream_len"] and hashlib.sha256(s).hexdigest() == c["stream_sha256"]
+    out, e = oracle.decompress(s, c["decode_out_len"])
+    assert out == v and e == c["decode_errno"]

@@ -1,0 +1,24 @@
+# round-4 GPU runner: `bash tools/gpu_r04.sh <step>...`; every step has its own
+# time limit and the first failure ends the call (no retries)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r04
+mkdir -p $O
+for st in "$@"; do
+  echo "== step $st $(date +%T)"
+  case $st in
+    tests)  timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread > $O/tests.log 2>&1; rc=$?
+            grep -E "PASSED|FAILED|ERROR|SKIPPED" $O/tests.log | tail -4; tail -3 $O/tests.log; [ $rc = 0 ] || exit 1 ;;
+    smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
+            grep -v amdgpu.ids $O/smoke.log | tail -3 ;;
+    bench)  timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit 1
+            tail -1 $O/bench.json | cut -c1-900 ;;
+    json4k) timeout -k 10 300 python bench.py --workload json4k --no-cpu > $O/json4k.json 2> $O/json4k.err || exit 1
+            tail -1 $O/json4k.json | cut -c1-600 ;;
+    dec)    timeout -k 10 400 python bench.py --mode decompress --no-cpu > $O/dec.json 2> $O/dec.err || exit 1
+            tail -1 $O/dec.json | cut -c1-600 ;;
+    mixed)  timeout -k 10 600 python bench.py --workload mixed16k --total 4194304 --steps 3 --no-cpu > $O/mixed.json 2> $O/mixed.err || exit 1
+            tail -1 $O/mixed.json | cut -c1-600 ;;
+    *) echo "unknown step $st"; exit 2 ;;
+  esac
+done
