@@ -228,24 +228,57 @@ long gb_mget_payload(const uint8_t *keys, const uint64_t *key_off, const uint32_
             ret = rc;
             goto done;
         }
-        /* a side-table length that was too small (stale): size the item by
-         * the pre-pass and decode it again (rare) */
-        for (uint32_t k = 0; k < m; k++) {
-            if (dl[k] || exact[k]) continue;
-            uint32_t sz = 0;
-            int32_t e = 0;
-            if (lzf_host_decoded_size_batch(vals, &ioff[k], &len[k], &sz, &e, 1, maxrequestsize) || !sz) continue;
-            uint8_t *b = realloc(dec, total + sz);
-            if (!b) {
+        /* side-table lengths that were too small (stale): every such item is
+         * sized by ONE pre-pass batch and decoded by ONE batch into slots
+         * appended to the arena (uo / ul / us are free to reuse now; sk maps
+         * them back to their items) */
+        uint32_t ns = 0;
+        for (uint32_t k = 0; k < m; k++)
+            if (!dl[k] && !exact[k]) ns++;
+        if (ns) {
+            int32_t *se = malloc(ns * sizeof *se);
+            uint64_t *so = malloc(ns * sizeof *so);
+            uint32_t *sl = malloc(ns * sizeof *sl), *sk = malloc(ns * sizeof *sk);
+            for (uint32_t k = 0, j = 0; sk && k < m; k++) {
+                if (dl[k] || exact[k]) continue;
+                uo[j] = ioff[k];
+                ul[j] = len[k];
+                sk[j++] = k;
+            }
+            int ok = se && so && sl && sk &&
+                     lzf_host_decoded_size_batch(vals, uo, ul, us, se, ns, maxrequestsize) == LZF_GPU_OK;
+            uint64_t add = 0;
+            for (uint32_t j = 0; ok && j < ns; j++) {
+                so[j] = total + add;
+                add += us[j];
+            }
+            uint8_t *b = ok && add ? realloc(dec, total + add) : NULL;
+            if (ok && add && !b) {
+                free(se);
+                free(so);
+                free(sl);
+                free(sk);
                 ret = LZF_GPU_ENOMEM;
                 goto done;
             }
-            dec = b;
-            const uint64_t o = total;
-            total += sz;
-            g_mget_staged = total;
-            if (lzf_host_decompress_batch(vals, &ioff[k], &len[k], dec, &o, &sz, &dl[k], &er[k], 1)) continue;
-            ooff[k] = o;
+            if (b) {
+                dec = b;
+                /* items that do not decode at all keep size 0 (us == 0) */
+                if (lzf_host_decompress_batch(vals, uo, ul, dec, so, us, sl, se, ns) == LZF_GPU_OK) {
+                    for (uint32_t j = 0; j < ns; j++) {
+                        if (!us[j] || !sl[j]) continue;
+                        dl[sk[j]] = sl[j];
+                        er[sk[j]] = 0;
+                        ooff[sk[j]] = so[j];
+                    }
+                    total += add;
+                    g_mget_staged = total;
+                }
+            }
+            free(se);
+            free(so);
+            free(sl);
+            free(sk);
         }
     }
     {

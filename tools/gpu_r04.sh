@@ -19,6 +19,17 @@ for st in "$@"; do
             tail -1 $O/dec.json | cut -c1-600 ;;
     mixed)  timeout -k 10 600 python bench.py --workload mixed16k --total 4194304 --steps 3 --no-cpu > $O/mixed.json 2> $O/mixed.err || exit 1
             tail -1 $O/mixed.json | cut -c1-600 ;;
+    abslab) AB_SEED=0x5EED0003 timeout -k 10 600 python -u tools/ab_compress.py 2 65536 262144 3 gibson_amd/liblzf_hip.so gibson_amd/liblzf_hip_slab.so > $O/abslab.txt 2>&1 || exit 1
+            cat $O/abslab.txt ;;
+    k3t)    for L in timing slabtiming; do LZF_HIP_LIB=$PWD/gibson_amd/liblzf_hip_$L.so timeout -k 10 300 python -u tools/k3_timing.py 2 65536 262144 > $O/k3t_$L.txt 2>&1 || exit 1; echo $L; cat $O/k3t_$L.txt; done ;;
+    ab:*)   # ab:<variant>[:<variant>] -- text64k configs[2] 256 K values, base vs variants (one process)
+            v=${st#ab:}; libs="gibson_amd/liblzf_hip.so"; for x in ${v//:/ }; do libs="$libs gibson_amd/liblzf_hip_$x.so"; done
+            AB_SEED=0x5EED0003 timeout -k 10 600 python -u tools/ab_compress.py 2 65536 262144 3 $libs > $O/ab_${v//:/_}.txt 2>&1 || exit 1
+            grep -v amdgpu.ids $O/ab_${v//:/_}.txt ;;
+    env:*)  # env:<kind>:<n>:<count>:<setting>:<setting>... -- ab_env.py (settings use , and =)
+            IFS=: read -r _ k nn c rest <<< "$st"; IFS=: read -ra sets <<< "$rest"
+            timeout -k 10 600 python -u tools/ab_env.py $k $nn $c 3 "${sets[@]}" > $O/env_${k}_${nn}.txt 2>&1 || exit 1
+            grep -v amdgpu.ids $O/env_${k}_${nn}.txt ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done

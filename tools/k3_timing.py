@@ -7,8 +7,8 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["LZF_HIP_LIB"] = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gibson_amd",
-                                         "liblzf_hip_timing.so")
+os.environ.setdefault("LZF_HIP_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                  "gibson_amd", "liblzf_hip_timing.so"))
 os.environ.setdefault("LZF_GPU_LANE_MIN", "0")
 import torch  # noqa: E402
 
@@ -19,7 +19,7 @@ L = gibson_amd.lib()
 L.lzf_gpu_debug_kt.argtypes = [ctypes.c_void_p, ctypes.c_int]
 buf = (ctypes.c_ulonglong * 16)()
 src = torch.empty(count * n, dtype=torch.uint8, device="cuda")
-gibson_amd.synth_fill(kind, 0x5EED0003, 0, 1, count, n, src)
+gibson_amd.synth_fill(kind, int(os.environ.get("AB_SEED", "0x5EED0003"), 0), 0, 1, count, n, src)
 off = torch.arange(count, dtype=torch.int64, device="cuda") * n
 ln = torch.full((count,), n, dtype=torch.int32, device="cuda")
 cap = torch.full((count,), n - 4, dtype=torch.int32, device="cuda")
