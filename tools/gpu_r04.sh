@@ -30,6 +30,12 @@ for st in "$@"; do
             IFS=: read -r _ k nn c rest <<< "$st"; IFS=: read -ra sets <<< "$rest"
             timeout -k 10 600 python -u tools/ab_env.py $k $nn $c 3 "${sets[@]}" > $O/env_${k}_${nn}.txt 2>&1 || exit 1
             grep -v amdgpu.ids $O/env_${k}_${nn}.txt ;;
+    host)   for w in "2 65536 65536" "1 4096 524288" "3 16384 131072"; do set -- $w
+              LZF_GPU_HOST_THREADS=16 timeout -k 10 400 python -u tools/host_path_bench.py $1 $2 $3 5 > $O/host_$1_$2.json 2> $O/host_$1_$2.err || exit 1
+              cut -c1-400 $O/host_$1_$2.json; done ;;
+    pmcmix) for c in FETCH_SIZE WRITE_SIZE; do
+              timeout -s KILL 600 rocprofv3 --pmc $c --output-format csv -d $O/pmc_mixed_$c -o run -- python3 bench.py --workload mixed16k --total 4194304 --steps 1 --warmup 0 --no-cpu > $O/pmc_mixed_$c.log 2>&1 || exit 1
+              tail -1 $O/pmc_mixed_$c.log | cut -c1-200; done ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
