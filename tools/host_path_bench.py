@@ -12,6 +12,7 @@ import sys
 import time
 
 import numpy as np
+import torch  # noqa: F401  (before the library: one HIP runtime in the process)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
