@@ -221,11 +221,7 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
             /* ---- B(t-1): the table wave ------------------------------------- */
             /* one lane-ordered exchange per window, in window (= position)
              * order, five windows per asm group; no exec masking */
-#ifdef KT_ABL_B
-            if (false) {
-#else
             if (t >= 1u && t <= nb) {
-#endif
                 const uint32_t k = t - 1u, B = KT_BLK * k;
                 const uint32_t *Sk = S + KT_BLK * (k & 1u);
                 uint16_t *Ok = O + KT_BLK * (k % 3u);
@@ -262,7 +258,7 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 const uint32_t k2 = min(x2 ? (uint32_t)__builtin_ctzll(x2) >> 3 : 8u, cav);
                 const uint32_t r1 = (cp - cq1 - 1u) | (kt_code(k1) << 13);
                 const uint32_t r2 = ((cp - cq2 - 1u) | (kt_code(k2) << 13)) << 16;
-                rec[dv_rec_at(cp)] = cq1 ? (r1 | (cq2 ? r2 : 0u)) : 0u;
+                rec[cp] = cq1 ? (r1 | (cq2 ? r2 : 0u)) : 0u;
             }
             /* ---- Q <- O of block t-3 ---------------------------------------- */
             if (t >= 3u && t - 3u < nb) {
@@ -310,16 +306,11 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
         else KT_TM(0);
         /* the step's loads: agreement bytes of C1 first, then the input of
          * block t + KT_PF, so a wait for the former never waits for it */
-#ifdef KT_ABL_C
-        l1 = l2 = 0u;
-#endif
         c_b1[CS] = ld8(l1);
         c_b2[CS] = ld8(l2);
         pf[PS] = ld8(lp);
         if (w) KT_TM(5);
-#ifndef KT_ABL_S
         __syncthreads();
-#endif
         if (w) KT_TM(6);
         else KT_TM(1);
 #ifdef KT_TIMING
@@ -382,29 +373,12 @@ __global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt,
 #ifndef K3_THREADS
 #define K3_THREADS 256u
 #endif
-#ifndef K3_CB
-#define K3_CB      16u          /* records per parse block: 64 bytes of one line (8: 32 bytes, 32: the whole line) */
-#endif
+#define K3_CB      16u          /* records per parse block: 64 bytes of one line (32, the whole line: no gain) */
 #ifndef K3_NRES
 #define K3_NRES    2u           /* candidate tests per loop iteration (2: 206.2 vs 210.8 ms for 1 + a memory-free one) */
 #endif
 #ifndef K3_RW
 #define K3_RW      32u          /* bitmap words kept in LDS per lane (power of two) */
-#endif
-#ifndef K3_PIECES
-#define K3_PIECES 1u            /* 16-byte extension pieces per side per iteration (diagnostic: 2, 4) */
-#endif
-#ifndef K3_SLAB_NOSTORE
-#define K3_SLAB_NOSTORE 0       /* diagnostic ablation: status words not stored (outputs wrong, timing only) */
-#endif
-#ifndef K3_SLAB_NOREC
-#define K3_SLAB_NOREC 0         /* diagnostic: a far status test does not load the candidate's record with it */
-#endif
-#ifndef K3_SB
-#define K3_SB      64u          /* K3_SLAB: block statuses kept in LDS per lane (power of two; 15 positions each) */
-#endif
-#ifndef K3_NOSTORE
-#define K3_NOSTORE 0        /* diagnostic: 1 = the output's 16-byte stores are skipped (timing only) */
 #endif
 #ifndef K3_LITMIN
 #define K3_LITMIN   8u       /* lanes of the wave that must take a free-literal trip for it to run */
@@ -529,49 +503,17 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
     uint32_t o = 1u, run = 0u, p = 0u; /* o, run: the reference's op and lit (src/lzf_c.c:113-143) */
     uint32_t cb = 0xFFFFFFE0u;         /* records [cb, cb + K3_CB) in C0..C3 (C4..C7) */
     uint4 C0 = W, C1 = W, C2 = W, C3 = W;
-#if K3_CB == 32
-    uint4 C4 = W, C5 = W, C6 = W, C7 = W;
-#endif
     /* record d of the block: a select tree over the block's words (a dynamic
      * index would put the block in scratch memory) */
     const auto pick = [&](uint32_t d) -> uint32_t {
         const bool b0 = d & 1u, b1 = d & 2u;
         const uint32_t c0 = b1 ? (b0 ? C0.w : C0.z) : (b0 ? C0.y : C0.x);
         const uint32_t c1 = b1 ? (b0 ? C1.w : C1.z) : (b0 ? C1.y : C1.x);
-#if K3_CB >= 16
         const uint32_t c2 = b1 ? (b0 ? C2.w : C2.z) : (b0 ? C2.y : C2.x);
         const uint32_t c3 = b1 ? (b0 ? C3.w : C3.z) : (b0 ? C3.y : C3.x);
         const uint32_t lo = (d & 8u) ? ((d & 4u) ? c3 : c2) : ((d & 4u) ? c1 : c0);
-#if K3_CB == 32
-        const uint32_t c4 = b1 ? (b0 ? C4.w : C4.z) : (b0 ? C4.y : C4.x);
-        const uint32_t c5 = b1 ? (b0 ? C5.w : C5.z) : (b0 ? C5.y : C5.x);
-        const uint32_t c6 = b1 ? (b0 ? C6.w : C6.z) : (b0 ? C6.y : C6.x);
-        const uint32_t c7 = b1 ? (b0 ? C7.w : C7.z) : (b0 ? C7.y : C7.x);
-        const uint32_t hi = (d & 8u) ? ((d & 4u) ? c7 : c6) : ((d & 4u) ? c5 : c4);
-        return (d & 16u) ? hi : lo;
-#else
         return lo;
-#endif
-#else
-        return (d & 4u) ? c1 : c0;
-#endif
     };
-#if K3_SLAB
-    /* status of p's block (cw, first position cb0) in flight; the last K3_SB
-     * blocks' statuses in LDS, every block's in its record block's last word */
-    uint32_t cw = 0u, curw = 0u, cb0 = 0u;
-    __shared__ uint16_t k3_ring[K3_SB][K3_THREADS];
-    uint16_t *const ring = &k3_ring[0][threadIdx.x];
-#define K3_RING(w_) ring[((w_) & (K3_SB - 1u)) * K3_THREADS]
-#define K3_FLUSH_TO(w_) ((void)0)
-#define K3_COMMIT(b_, s_)                                                          \
-    do {                                                                           \
-        const uint32_t s__ = (s_);                                                 \
-        K3_RING(b_) = (uint16_t)s__;                                               \
-        if (!K3_SLAB_NOSTORE) const_cast<uint32_t *>(rec)[16u * (b_) + 15u] = s__; \
-    } while (0)
-    (void)bits;
-#else
     uint32_t cw = 0u, curw = 0u;       /* inserted-bitmap word of p, in flight */
     __shared__ uint32_t k3_ring[K3_RW][K3_THREADS];
     uint32_t *const ring = &k3_ring[0][threadIdx.x];
@@ -585,7 +527,6 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
             fl += 4u;                                                              \
         }                                                                          \
     } while (0)
-#endif
     uint32_t ms = 0u, me = 0u;         /* the last match: [ms, me) */
     uint32_t rel = 0u, q = 0u, k = 0u, lim = 0u, m = 0u;
     uint32_t reln = 0u, qn = 0u;       /* the next chain link from the same record (reln 0: none) */
@@ -614,8 +555,7 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
             __builtin_memcpy(da + 12u, &l_, 4);                                    \
         } else {                                                                   \
             const uint4 v_ = make_uint4(pb0, pb1, pb2, (w_));                      \
-            if (!K3_NOSTORE || bt.max_len == 0xFFFFFFFFu)                          \
-                __builtin_memcpy(da + 4u * fs, &v_, 16);                           \
+            __builtin_memcpy(da + 4u * fs, &v_, 16);                               \
         }                                                                          \
     } while (0)
 #define K3_PUT(bytes_, cnt_)                                                       \
@@ -681,41 +621,15 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
             } else {
                 K3_CNT(10);
                 uint32_t d = p - cb;
-#if K3_SLAB
-                if (d >= 15u) {
-                    K3_CNT(15);
-                    const uint32_t bb_ = dv_blk15(p);
-                    cb = 15u * bb_;
-                    d = p - cb;
-                    const uint4 *cp = (const uint4 *)(rec + 16u * bb_);
-#else
                 if (d >= K3_CB) {
                     K3_CNT(15);
                     cb = p & ~(K3_CB - 1u);
                     d = p - cb;
                     const uint4 *cp = (const uint4 *)(rec + cb);
-#endif
-#ifdef K3_DUPBLK    /* diagnostic: a second line per record block, same wait */
-                    {
-                        const uint32_t db_ = cb >= 64u ? cb - 64u : cb + 64u;
-                        const uint4 d_ = *(const uint4 *)(rec + db_);
-                        C0 = cp[0];
-                        C0.x |= d_.x & bt.max_len & 0x80000000u;
-                    }
-#else
                     C0 = cp[0];
-#endif
                     C1 = cp[1];
-#if K3_CB >= 16
                     C2 = cp[2];
                     C3 = cp[3];
-#endif
-#if K3_CB == 32
-                    C4 = cp[4];
-                    C5 = cp[5];
-                    C6 = cp[6];
-                    C7 = cp[7];
-#endif
                 }
                 const uint32_t c = pick(d);
                 rel = (c >> 13) & 7u;
@@ -733,50 +647,16 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
             if (mode == K3_RESOLVE) {
                 K3_CNT(11);
                 uint32_t word;
-#if K3_SLAB
-                uint32_t qrec = 0u;            /* q's record, loaded with a far status word */
-                bool qhave = false;
-                uint32_t qbit = 0u;            /* the last match's words are all-0 or all-1 */
-#endif
                 if (q >= ms) {
                     word = (q > ms && q + 3u <= me) ? 0u : 0xFFFFFFFFu;         /* last match's interior */
                 } else {
-#if K3_SLAB
-                    const uint32_t bq = dv_blk15(q), d = cw - bq;
-                    qbit = q - 15u * bq;
-                    if (d == 0u) {
-                        word = curw;
-                    } else if (d <= K3_SB) {
-                        word = K3_RING(bq);
-                    } else {
-                        /* the status word and q's record: one line, one wait */
-                        K3_CNT(12);
-                        const uint32_t *blk = rec + 16u * bq;
-                        word = blk[15];
-                        if (!K3_SLAB_NOREC) {
-                            qrec = blk[qbit];
-                            qhave = true;
-                        }
-                    }
-                }
-                if ((word >> qbit) & 1u) {                                   /* q is the ref */
-#else
                     const uint32_t d = cw - (q >> 5);
-#ifdef K3_DUPBITS   /* diagnostic: a second line per scratch bitmap word, same wait */
-                    if (d != 0u && (q >> 5) < fl) {
-                        const uint32_t x_ = bits[(q >> 5) ^ 64u];
-                        word = bits[q >> 5] | (x_ & bt.max_len & 0x80000000u);
-                    } else
-                        word = d == 0u ? curw : K3_RING(q >> 5);
-#else
                     word = d == 0u ? curw : (q >> 5) >= fl ? K3_RING(q >> 5) : bits[q >> 5];
-#endif
 #ifdef KT_TIMING
                     if (d && (q >> 5) < fl) K3_CNT(12);
 #endif
                 }
                 if ((word >> (q & 31u)) & 1u) {                              /* q is the ref */
-#endif
                     if (rel == 9u) {
                         /* bytes q..q+2 against p..p+2 with one 4-byte load per side
                          * (q + 3 <= p + 2 < n and p >= 1: both inside the value),
@@ -786,43 +666,15 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
                     }
                     mode = K3_DECIDE;
                 } else if (reln) {                                           /* the record's second link */
-#if K3_SLAB
-                    if (qhave) {
-                        /* q's record came with its status: q's first link is qn,
-                         * its second the link after qn -- no load later */
-                        const uint32_t r2 = qrec >> 29, y2 = q - 1u - ((qrec >> 16) & 0x1FFFu);
-                        const uint32_t rq = rel;
-                        q = qn;
-                        rel = reln;
-                        if (r2 && p - y2 - 1u < LZF_WINDOW && ((qrec >> 13) & 7u)) {
-                            reln = k3_comb(rq, r2);
-                            qn = y2;
-                        } else {
-                            reln = 0u;
-                            qn = 0u;                                         /* nothing after qn */
-                        }
-                    } else
-#endif
-                    {
                     q = qn;
                     rel = reln;
                     reln = 0u;
                     /* the link after it needs q's own record: mark with reln 0 and
                      * qn = q (a load below on the next failure) */
                     qn = 0xFFFFFFFFu;
-                    }
                 } else if (qn == 0xFFFFFFFFu) {                              /* load q's record: two more links */
-#if K3_SLAB
-                    if (!qhave) K3_CNT(13);
-                    const uint32_t c2 = qhave ? qrec : rec[dv_rec_at(q)];
-#else
                     K3_CNT(13);
-#ifdef K3_DUPREC    /* diagnostic: a second line per record hop, same wait */
-                    const uint32_t c2 = rec[q] | (rec[q ^ 64u] & bt.max_len & 0x80000000u);
-#else
                     const uint32_t c2 = rec[q];
-#endif
-#endif
                     const uint32_t r1 = (c2 >> 13) & 7u, r2 = c2 >> 29;
                     const uint32_t y1 = q - 1u - (c2 & 0x1FFFu), y2 = q - 1u - ((c2 >> 16) & 0x1FFFu);
                     if (!r1 || p - y1 - 1u >= LZF_WINDOW) {                  /* the chain leaves p's window */
@@ -848,11 +700,7 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
         }
         /* ---- literal, or the start of a back-reference --------------------- */
         if (mode == K3_DECIDE) {
-#if K3_SLAB
-            curw |= 1u << (p - cb0);                                     /* p is inserted */
-#else
             curw |= 1u << (p & 31u);                                     /* p is inserted */
-#endif
             if (!(rel >= 2u && p + 4u < n)) {                            /* src/lzf_c.c:151-166 */
                 if (o >= cap) {                                          /* src/lzf_c.c:263 */
                     ok = false;
@@ -860,21 +708,12 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
                 } else {
                     K3_LITERAL(p);
                     p++;
-#if K3_SLAB
-                    if (p == cb0 + 15u) {
-                        K3_COMMIT(cw, curw);
-                        cw++;
-                        cb0 += 15u;
-                        curw = 0u;
-                    }
-#else
                     if ((p & 31u) == 0u) {
                         K3_FLUSH_TO(cw);
                         K3_RING(cw) = curw;
                         cw++;
                         curw = 0u;
                     }
-#endif
                     mode = K3_STEP;
 #if K3_LITX
                     /* free literals (lzf_lane.hip's parse has the same path):
@@ -899,11 +738,7 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
                          * wait through it */
                         if ((uint32_t)__builtin_popcountll(__ballot(go)) < K3_LITMIN) break;
                         if (go) {
-#if K3_SLAB
-                            curw |= 1u << (p - cb0);
-#else
                             curw |= 1u << (p & 31u);
-#endif
                             const uint32_t byte_ = (dv_sel4(W, x_ >> 2) >> (8u * (x_ & 3u))) & 0xFFu;
                             const bool first_ = run == 0u;
                             hx = first_ ? 4u * fw + accn : hx;
@@ -911,21 +746,12 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
                             o++;
                             if (++run == LZF_MAX_LIT) { K3_PATCH(hx, LZF_MAX_LIT - 1u); run = 0u; o++; }
                             p++;
-#if K3_SLAB
-                            if (p == cb0 + 15u) {
-                                K3_COMMIT(cw, curw);
-                                cw++;
-                                cb0 += 15u;
-                                curw = 0u;
-                            }
-#else
                             if ((p & 31u) == 0u) {
                                 K3_FLUSH_TO(cw);
                                 K3_RING(cw) = curw;
                                 cw++;
                                 curw = 0u;
                             }
-#endif
                         }
                     }
 #endif
@@ -946,59 +772,17 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
         }
         /* ---- one 16-byte piece of a long match ----------------------------- */
         if (mode == K3_EXTEND) {
-#if K3_PIECES > 1
-            /* diagnostic: K3_PIECES 16-byte pieces per side per iteration, the
-             * loads issued together (one wait) */
-            if (k < lim) {
-                K3_CNT(14);
-                uint4 a_[K3_PIECES], b_[K3_PIECES];
-#pragma unroll
-                for (uint32_t i_ = 0; i_ < K3_PIECES; i_++) {
-                    const uint32_t kk_ = k + 16u * i_;
-                    const uint32_t av_ = kk_ < n - p ? n - (p + kk_) : 0u;
-                    const bool in_ = kk_ < lim;
-                    a_[i_] = in_ ? dv_ld16_safe(src + p + kk_, av_) : make_uint4(0, 0, 0, 0);
-                    b_[i_] = in_ ? dv_ld16_safe(src + q + kk_, av_) : make_uint4(0, 0, 0, 0);
-                }
-                uint32_t d = 0u;
-                bool run_ = true;
-#pragma unroll
-                for (uint32_t i_ = 0; i_ < K3_PIECES; i_++) {
-                    if (run_) {
-                        const uint32_t e_ = dv_first_diff(a_[i_], b_[i_]);
-                        d += e_;
-                        run_ = e_ == 16u;
-                        if (k + 16u * i_ < lim) {        /* a loaded piece: literals after the match read it */
-                            W = a_[i_];
-                            wb = p + k + 16u * i_;
-                        }
-                    }
-                }
-                k += d;
-                if (!run_) lim = k < lim ? k : lim;
-            }
-#else
             if (k < lim) {
                 K3_CNT(14);
                 const uint32_t avail = n - (p + k);
                 const uint4 a = dv_ld16_safe(src + p + k, avail);
-#ifdef K3_DUPEXT    /* diagnostic: a second line per extension piece's q side, same wait */
-                uint4 b = dv_ld16_safe(src + q + k, avail);
-                {
-                    const uint32_t qd_ = (q + k) >= 256u ? q + k - 256u : q + k + 256u;
-                    const uint4 d_ = dv_ld16(src + (qd_ < n - 16u ? qd_ : 0u));
-                    b.x |= d_.x & bt.max_len & 0x80000000u;
-                }
-#else
                 const uint4 b = dv_ld16_safe(src + q + k, avail);
-#endif
                 W = a;                                   /* literals after the match read it */
                 wb = p + k;
                 const uint32_t d = dv_first_diff(a, b);
                 k += d;
                 if (d < 16u) lim = k < lim ? k : lim;
             }
-#endif
             if (k >= lim) {
                 m = lim;
                 mode = K3_EMIT;
@@ -1028,24 +812,6 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
                     mode = K3_DONE;
                 } else {
                     /* the two last positions of the match are inserted, its interior not */
-#if K3_SLAB
-                    const uint32_t nw = dv_blk15(p), t1 = p - 2u, t2 = p - 1u;
-                    const uint32_t w1 = dv_blk15(t1), w2 = dv_blk15(t2);
-                    const uint32_t b1 = 1u << (t1 - 15u * w1), b2 = 1u << (t2 - 15u * w2);
-                    if (nw == cw) {
-                        curw |= b1 | b2;
-                    } else {
-                        const uint32_t wo = curw | (w1 == cw ? b1 : 0u) | (w2 == cw ? b2 : 0u);
-                        const uint32_t wn = (w1 == nw ? b1 : 0u) | (w2 == nw ? b2 : 0u);
-                        const uint32_t wm = (w1 != cw && w1 != nw ? b1 : 0u) | (w2 != cw && w2 != nw ? b2 : 0u);
-                        K3_COMMIT(cw, wo);
-                        /* blocks cw+1 .. nw-2 are all interior (0), nw-1 holds tails */
-                        for (uint32_t w = cw + 1u; w < nw; w++) K3_COMMIT(w, w + 1u == nw ? wm : 0u);
-                        curw = wn;
-                        cw = nw;
-                        cb0 = 15u * nw;
-                    }
-#else
                     const uint32_t nw = p >> 5, t1 = p - 2u, t2 = p - 1u;
                     const uint32_t b1 = 1u << (t1 & 31u), b2 = 1u << (t2 & 31u);
                     if (nw == cw) {
@@ -1065,7 +831,6 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
                         curw = wn;
                         cw = nw;
                     }
-#endif
                     mode = K3_STEP;
                 }
             }
@@ -1107,26 +872,17 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
 #undef K3_LITERAL
 #undef K3_RING
 #undef K3_FLUSH_TO
-#if K3_SLAB
-#undef K3_COMMIT
-#endif
 }
 
 /* ---- launcher ------------------------------------------------------------ */
 
 /* records per value: a multiple of 16 (64 bytes) plus one block of slack, so
  * the parse's 64-byte blocks never straddle a line and never leave the value */
-#if K3_SLAB
-/* 16 words per 15 positions, plus one block of slack */
-static uint64_t rec_stride(uint32_t max_len) { return 16u * (((uint64_t)max_len + 14u) / 15u) + 16u; }
-static uint64_t rec_bstride(uint32_t) { return 0u; }
-#else
 static uint64_t rec_stride(uint32_t max_len)
 {
     return (((uint64_t)max_len + K3_CB - 1u) & ~(uint64_t)(K3_CB - 1u)) + (K3_CB < 16u ? 16u : K3_CB);
 }
 static uint64_t rec_bstride(uint32_t max_len) { return ((((uint64_t)max_len + 31u) >> 5) + 3u) & ~3ull; }
-#endif
 
 size_t lzf_table_scratch_per_value(uint32_t max_len)
 {

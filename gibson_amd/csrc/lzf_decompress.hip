@@ -54,35 +54,14 @@
 #ifndef CD_OUT_MAX
 #define CD_OUT_MAX 8192u
 #endif
-/* token discovery: 1 = the scalar walk over size-2 runs, 0 = pointer doubling */
-#ifndef CD_WALK
-#define CD_WALK    0
-#endif
-/* step 4: 1 = groups inside one long token copy without the owner search.
- * Measured slower on every shape (same-process A/B, 5 rounds: sentence text
- * 128 K x 64 KiB 16.02 -> 17.83 ms, Zipf 1 M x 8 KiB 20.05 -> 21.05, json
- * 1 M x 4 KiB 7.47 -> 7.91, mixed 256 K x 16 KiB 11.48 -> 11.89): the per-round
- * check and the per-group readlanes sit on the consumer's critical path and
- * cost more than the owner search they skip.  Off. */
-#ifndef CD_WHOLE
-#define CD_WHOLE   0
-#endif
-/* step 4: 1 = the next group's owner search issued while the current group's
- * bytes are read (two serial LDS round trips per group instead of three).
- * Slower (same-process A/B, 5 rounds: sentence text 128 K x 64 KiB 15.84 ->
- * 16.19 ms, Zipf 1 M x 8 KiB 19.85 -> 20.13, json 7.46 -> 7.60, mixed 11.45 ->
- * 11.67): with 8 waves per SIMD the consumer is bound by instruction issue,
- * not by its LDS round trips.  Off. */
-#ifndef CD_PIPEG
-#define CD_PIPEG   0
-#endif
-static_assert(!(CD_WHOLE && CD_PIPEG), "the whole-token path keeps tbase per group");
-/* step 4's stores: 1 = completed output leaves the LDS window in 16-byte
- * pieces per lane, a flush unit (1 KiB, or half the window) at a time; 0 =
- * one global byte store per lane per 64-byte group */
-#ifndef CD_WIDE
-#define CD_WIDE    1
-#endif
+/* Measured and removed (same-process A/Bs, all bit-exact):
+ * a scalar walk over size-2 runs for token discovery (no faster); groups
+ * inside one long token copied without the owner search (slower on every
+ * shape: the per-round check and per-group readlanes sit on the consumer's
+ * critical path); the next group's owner search overlapped with the current
+ * group's byte reads (slower: the consumer is issue-bound at 8 waves per
+ * SIMD).  Kept: completed output leaves the LDS window in 16-byte pieces per
+ * lane, a flush unit (1 KiB, or half the window) at a time. */
 /* decoder form: 1 = pipe (producer + consumer wave per stream), 0 = tokpar64 */
 #ifndef CD_PIPE
 #define CD_PIPE    1
@@ -184,54 +163,6 @@ __device__ __forceinline__ uint32_t cd_discover(const uint8_t *inr, uint32_t ima
     const uint32_t pa = 2u * lane, pb = pa + 1u;
     const uint32_t ca = inr[(base + pa) & imask], cb = inr[(base + pb) & imask];
     const uint32_t ta = cd_tsz(ca), tb = cd_tsz(cb);
-#if CD_WALK
-    /* a scalar walk: the 2-byte back-references (the bulk of a stream) become
-     * two lane masks, one per parity, so a run of them is skipped in one step
-     * and only literals and 3-byte back-references are stepped over one by
-     * one.  Tokens start at the walk's positions below lim; the first token
-     * is decoded even from an empty stream (src/lzf_d.c:64 is a do-while) */
-    uint32_t lim = in_len > base ? in_len - base : 0u;
-    if (lim > CD_ROUND) lim = CD_ROUND;
-    if (lim == 0u) lim = 1u;
-    const uint64_t E2 = __ballot(ta == 2u && pa < lim);
-    const uint64_t O2 = __ballot(tb == 2u && pb < lim);
-    const uint32_t tsz2 = ta | (tb << 8);
-    uint64_t SE = 0ull, SO = 0ull;
-    uint32_t pos = 0;
-    /* one branch per parity keeps the masks out of selects; a run from bit j
-     * of mask m is the bits below the lowest clear bit of y = m >> j */
-    for (;;) {
-        const uint32_t j = pos >> 1;
-        if (pos & 1u) {
-            const uint64_t y = O2 >> j;
-            const uint64_t run = (~y & (y + 1ull)) - 1ull;
-            SO |= run << j;
-            pos += 2u * (uint32_t)__builtin_popcountll(run);
-            if (pos >= lim) break;
-            SO |= 1ull << (pos >> 1);
-            pos += cd_rl(tsz2, pos >> 1) >> 8;
-        } else {
-            const uint64_t y = E2 >> j;
-            const uint64_t run = (~y & (y + 1ull)) - 1ull;
-            SE |= run << j;
-            pos += 2u * (uint32_t)__builtin_popcountll(run);
-            if (pos >= lim) break;
-            SE |= 1ull << (pos >> 1);
-            pos += cd_rl(tsz2, pos >> 1) & 0xFFu;
-        }
-        if (pos >= lim) break;
-    }
-    nbase = base + pos;
-    /* lane l takes the l-th start: ranks by mbcnt, scattered through LDS */
-    const bool sa = (SE >> lane) & 1ull, sb = (SO >> lane) & 1ull;
-    const uint32_t ra = __builtin_amdgcn_mbcnt_hi((uint32_t)(SE >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)SE, 0u)) +
-                        __builtin_amdgcn_mbcnt_hi((uint32_t)(SO >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)SO, 0u));
-    if (sa) tokpos[ra] = (uint8_t)pa;
-    if (sb) tokpos[ra + (sa ? 1u : 0u)] = (uint8_t)pb;
-    cd_fence();
-    const uint32_t nt = (uint32_t)__builtin_popcountll(SE) + (uint32_t)__builtin_popcountll(SO);
-    return lane < nt ? tokpos[lane] : CD_ROUND;
-#else
     (void)tokpos;
     /* jump tables J0..J5 over the round's 128 positions packed two per lane
      * as bytes (bits 0-7: position 2l, 8-15: 2l + 1).  Leaving the round is
@@ -268,7 +199,6 @@ __device__ __forceinline__ uint32_t cd_discover(const uint8_t *inr, uint32_t ima
     const uint32_t c = inr[(base + (tok ? x : 0u)) & imask];
     nbase = base + cd_rl(x + cd_tsz(c), ntok - 1u);
     return x;
-#endif
 }
 
 /* steps 2-3 for lane l's token: its output offset within the round (rel),
@@ -360,69 +290,17 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
                                              uint32_t sink_off, uint8_t *dst, uint32_t O, uint32_t total, bool tok,
                                              uint32_t Ot, uint32_t tinfo, uint32_t lane, uint32_t &F)
 {
-    /* CD_WIDE: a flush unit of the window's completed bytes goes out as soon
+    /* a flush unit of the window's completed bytes goes out as soon
      * as it is complete (half the window at most, so no byte is overwritten
      * before it is stored) */
-#if CD_WIDE
     const uint32_t unit = (omask + 1u) / 2u < 1024u ? (omask + 1u) / 2u : 1024u;
-#else
-    (void)F;
-#endif
     constexpr uint32_t imask = IN_RING - 1u;
     uint32_t tbase = 0;          /* tokens started before the group */
 #ifdef LZF_CD_ABLATE_OUTPUT           /* diagnostic builds only: time discovery alone */
     total = 0u;
 #endif
-#if CD_WHOLE
-    /* whole-token groups: a group that lies inside one token whose bytes all
-     * come from before the group (a literal, or a back-reference reaching 64
-     * or more back) needs no owner search and no doubling -- every lane copies
-     * its byte from the source address the token gives.  Checked per group
-     * only when the round has such a token of >= 64 bytes. */
-    const uint64_t TK = __ballot(tok);
-    const uint32_t ntok = (uint32_t)__builtin_popcountll(TK);
-    const uint32_t onext = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane + 1u) << 2), (int)Ot);
-    const uint32_t tlen = (lane + 1u < ntok ? onext : O + total) - Ot;
-    const bool whole_any = __ballot(tok && tlen >= CD_LANES && ((int32_t)tinfo < 0 || tinfo >= CD_LANES)) != 0ull;
-#endif
-#if CD_PIPEG
-    /* the owner info of every byte of group g: marks of the token starts in
-     * the group (tagged gb + 1), one ballot, and the owner's word */
-    const auto owner = [&](uint32_t g) -> uint32_t {
-        const uint32_t gb = O + g;
-        if (tok && Ot - gb < CD_LANES) mark[Ot - gb] = gb + 1u;
-        cd_fence();
-        const uint64_t S = __ballot(mark[lane] == gb + 1u);
-        const uint32_t le = __builtin_amdgcn_mbcnt_hi((uint32_t)(S >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)S, 0u)) +
-                            (uint32_t)((S >> lane) & 1ull);
-        const uint32_t k = tbase + le - 1u;
-        tbase += (uint32_t)__builtin_popcountll(S);
-        return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)tinfo);
-    };
-    uint32_t tI = total ? owner(0u) : 0u;
-#endif
     for (uint32_t g = 0; g < total; g += CD_LANES) {
         const uint32_t gb = O + g;                     /* group's first output offset */
-#if CD_WHOLE
-        if (whole_any && tbase > 0u && g + CD_LANES <= total) {
-            /* the next token to start, relative to O (total: none left) */
-            const uint32_t ns = tbase < ntok ? cd_rl(Ot, tbase) - O : total;
-            const uint32_t ti = cd_rl(tinfo, tbase - 1u);
-            if (ns >= g + CD_LANES && ((int32_t)ti < 0 || ti >= CD_LANES)) {
-                const uint32_t o = gb + lane;
-                const uint32_t a = (int32_t)ti < 0 ? ((o + ti) & imask) : outr_off + ((o - ti) & omask);
-                const uint32_t b = lds[a];
-                lds[outr_off + (o & omask)] = (uint8_t)b;
-                dst[o] = (uint8_t)b;
-                cd_fence();
-                continue;
-            }
-        }
-#endif
-#if CD_PIPEG
-        const uint32_t tInf = tI;
-#else
         if (tok && Ot - gb < CD_LANES) mark[Ot - gb] = gb + 1u;
         cd_fence();
         const uint64_t S = __ballot(mark[lane] == gb + 1u);
@@ -432,25 +310,17 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
         const uint32_t k = tbase + le - 1u;
         tbase += (uint32_t)__builtin_popcountll(S);
         const uint32_t tInf = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)tinfo);
-#endif
         const uint32_t o = gb + lane;
         const uint32_t lit = (uint32_t)((int32_t)tInf >> 31);
         const uint32_t so = o - tInf;
         const uint32_t a = (((o + tInf) & imask) & lit) | ((outr_off + (so & omask)) & ~lit);
         const uint32_t q = so - gb;
         const uint32_t b = lds[a];
-#if CD_PIPEG
-        /* the next group's owners while this group's bytes are in flight (its
-         * byte reads come after this group's writes: one wave's LDS operations
-         * execute in order) */
-        const uint32_t tIn = g + CD_LANES < total ? owner(g + CD_LANES) : 0u;
-#endif
         uint32_t ent = (!lit && q < CD_LANES) ? (q << 8) : (0x10000u | b);
         while (__ballot(!(ent & 0x10000u)))
             ent = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((ent & 0x10000u) ? lane : (ent >> 8)) << 2), (int)ent);
         const bool live = g + lane < total;
         lds[live ? outr_off + (o & omask) : sink_off] = (uint8_t)ent;
-#if CD_WIDE
         cd_fence();
         {
             const uint32_t done = g + CD_LANES <= total ? gb + CD_LANES : O + total;
@@ -465,14 +335,6 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
                 F += unit;
             }
         }
-#else
-        if (g + CD_LANES <= total) dst[o] = (uint8_t)ent;
-        else if (live) dst[o] = (uint8_t)ent;
-        cd_fence();
-#endif
-#if CD_PIPEG
-        tI = tIn;
-#endif
     }
 }
 
@@ -508,7 +370,7 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
 
     mark[lane] = 0u;            /* group tags are >= 1 */
     uint32_t loaded = 0, base = 0, O = 0;
-    uint32_t F = 0;             /* output [0, F) stored (CD_WIDE) */
+    uint32_t F = 0;             /* output [0, F) stored */
     int32_t err = 0;
     bool first = true;
     while (first || base < in_len) {                     /* src/lzf_d.c:64, 146 */
@@ -526,9 +388,7 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
         O += r.total;
         base = nbase;
     }
-#if CD_WIDE
     cd_flush(smem, CD_IN_RING1, omask, dst, F, O, lane);   /* the rounds before a failing one, as the reference */
-#endif
     if (lane == 0) {
         bt.out_len[v] = err ? 0u : O;
         bt.err[v] = err;
@@ -570,7 +430,7 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
     uint8_t *inr = smem;                               /* CD_IN_RINGP */
     CdSlot *slot = (CdSlot *)(smem + CD_IN_RINGP);     /* 2 */
     uint32_t *mark = (uint32_t *)(slot + 2);           /* the consumer's 64 token-start marks */
-    uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* the walk's token starts (CD_WALK, producer) */
+    uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* unused (was the removed walk's token starts) */
     uint8_t *sink = tokpos + CD_LANES;                 /* the consumer's idle-lane byte sink */
     uint8_t *outr = sink + 16u;                        /* out_ring (power of two) */
     const uint32_t imask = CD_IN_RINGP - 1u, omask = out_ring - 1u;
@@ -615,7 +475,7 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
         }
     } else {
         uint8_t *dst = bt.out + bt.out_off[v];
-        uint32_t O = 0, F = 0;  /* output [0, F) stored (CD_WIDE) */
+        uint32_t O = 0, F = 0;  /* output [0, F) stored */
         int32_t err = 0;
         mark[lane] = 0u;        /* group tags are >= 1 */
         cd_barrier();
@@ -634,9 +494,7 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
             if (last) break;
             cd_barrier(tw);
         }
-#if CD_WIDE
         cd_flush(smem, (uint32_t)(outr - smem), omask, dst, F, O, lane);   /* also before a failing round */
-#endif
 #ifdef CD_TIMING
         tw[0] += __builtin_amdgcn_s_memtime() - tw[2];
 #endif

@@ -83,28 +83,6 @@ __device__ __forceinline__ uint4 dv_shr16(uint4 v, uint32_t sh)
     return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
-/* Record layout of the table generation (lzf_cand.hip).  K3_SLAB = 1: each
- * 64-byte block holds the records of 15 positions and, in its last word, the
- * inserted status of those positions (written by the parse as it passes
- * them), so a candidate's status and its record -- the next chain links --
- * come from one line.  K3_SLAB = 0: records back to back, the status in a
- * separate bitmap. */
-#ifndef K3_SLAB
-#define K3_SLAB 0
-#endif
-/* x / 15 for x < 70000 (checked exhaustively) */
-__device__ __forceinline__ uint32_t dv_blk15(uint32_t x) { return (x * 34953u) >> 19; }
-/* word index of position x's record */
-__device__ __forceinline__ uint32_t dv_rec_at(uint32_t x)
-{
-#if K3_SLAB
-    const uint32_t b = dv_blk15(x);
-    return 16u * b + (x - 15u * b);
-#else
-    return x;
-#endif
-}
-
 /* slot(p) of src/lzf_c.c:47-57 (VERY_FAST, HLOG 16) from b[p..p+2] = tri */
 __device__ __forceinline__ uint32_t dv_slot(uint32_t tri)
 {

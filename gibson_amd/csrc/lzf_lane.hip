@@ -527,9 +527,6 @@ __global__ __launch_bounds__(64) void lzf_cand_small_kernel(LzfBatch bt, LzfLane
                     need |= cur[j] != 0u;
                 }
                 ln_wave_fence();
-#ifdef KS_ABL_WALK
-                need = false;
-#endif
                 while (__ballot(need)) {
                     need = false;
 #pragma unroll
@@ -931,17 +928,8 @@ extern "C" int lzf_gpu_debug_sites(unsigned long long *out16, int reset)
 #ifndef K2_NRES
 #define K2_NRES 1u
 #endif
-#ifndef K2_NOSTORE
-#define K2_NOSTORE 0        /* diagnostic: 1 = the output's 16-byte stores are skipped (timing only) */
-#endif
 #ifndef K2_LITMIN
 #define K2_LITMIN   8u       /* lanes of the wave that must take a free-literal trip for it to run */
-#endif
-#ifndef K2_LITPRE
-#define K2_LITPRE   K2_LITMIN   /* lanes of the wave that must be at a literal for the path to run */
-#endif
-#ifndef K2_LITUNG
-#define K2_LITUNG   0u       /* trips taken without the per-trip gate */
 #endif
 #ifndef K2_LITX
 #define K2_LITX 3u       /* free literals taken after a literal in the same iteration (0: none) */
@@ -1015,8 +1003,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
             __builtin_memcpy(da + 12u, &l_, 4);                                    \
         } else {                                                                   \
             const uint4 v_ = make_uint4(pb0, pb1, pb2, (w_));                      \
-            if (!K2_NOSTORE || bt.max_len == 0xFFFFFFFFu)                          \
-                __builtin_memcpy(da + 4u * fs, &v_, 16);                           \
+            __builtin_memcpy(da + 4u * fs, &v_, 16);                               \
         }                                                                          \
         K2_SITE(8);                                                                \
     } while (0)
@@ -1172,7 +1159,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                      * all (one ballot of the branch's lanes): on text, where
                      * few are, the wave skips the path */
                     bool go = true;
-                    if ((uint32_t)__builtin_popcountll(__ballot(true)) >= K2_LITPRE)
+                    if ((uint32_t)__builtin_popcountll(__ballot(true)) >= K2_LITMIN)
 #pragma unroll
                     for (uint32_t e_ = 0; e_ < K2_LITX; e_++) {
                         const uint32_t d_ = p - cb, x_ = p - wb;
@@ -1185,7 +1172,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                         /* a trip the wave takes only when enough lanes gain
                          * from it: on text, where few do, the others would
                          * wait through it */
-                        if (e_ >= K2_LITUNG && (uint32_t)__builtin_popcountll(__ballot(go)) < K2_LITMIN) break;
+                        if ((uint32_t)__builtin_popcountll(__ballot(go)) < K2_LITMIN) break;
                         if (go) {
                             K2_SITE(9);
                             curw |= 1u << (p & 31u);

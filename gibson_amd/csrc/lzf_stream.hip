@@ -33,9 +33,6 @@
 #define KS_THR    (64u * (KS_WINS + 1u))
 #define KS_PF     4u                         /* blocks of input in flight (the step loop's unroll) */
 #define KS_CL     2u                         /* steps from the agreement load to its use */
-#ifndef KS_OPT
-#define KS_OPT    1                          /* byte shifts only near a value's end; p's slot carried from A to C2 */
-#endif
 
 __device__ __forceinline__ uint32_t ks_lds_addr(const void *p)
 {
@@ -347,12 +344,7 @@ __global__ __launch_bounds__(KS_THR) void lzf_cand_stream_kernel(LzfBatch bt, ui
                         xd[i] = e.y;
                     }
                 }
-#ifdef KS_ABL_B     /* diagnostics: no exchanges (outputs wrong) */
-#pragma unroll
-                for (uint32_t i = 0; i < 15u; i++) xr[i] = xd[i];
-#else
                 ks_xchg15(xr, xa, xm, xd);
-#endif
 #pragma unroll
                 for (uint32_t i = 0; i < 15u; i++) Ok[64u * i + lane] = (uint16_t)(xr[i] >> hs[i]);
             }
@@ -362,17 +354,11 @@ __global__ __launch_bounds__(KS_THR) void lzf_cand_stream_kernel(LzfBatch bt, ui
             if (c_p[CS] != 0xFFFFFFFFu) {
                 const uint32_t p = c_p[CS], q = c_q[CS], n = c_n[CS];
                 const uint2 a = c_a[CS];
-#if KS_OPT
                 /* no lane within 8 bytes of its value's end: every q < p too,
                  * so the loads were not moved back and need no shift */
                 const bool near_end = __ballot(p + 8u > n) != 0ull;
                 const uint2 b = near_end ? ks_fix(c_b[CS], n, q) : c_b[CS];
                 const uint32_t sp = c_s[CS];
-#else
-                const bool near_end = true;
-                const uint2 b = ks_fix(c_b[CS], n, q);
-                const uint32_t sp = dv_slot(a.x);
-#endif
                 /* branch-free (every branch costs the wave its exec-mask
                  * juggling): both tests always, the word by selects.  q1: a
                  * stale table entry names a position of another slot */
@@ -417,9 +403,7 @@ __global__ __launch_bounds__(KS_THR) void lzf_cand_stream_kernel(LzfBatch bt, ui
                     c_p[CS] = p;
                     c_q[CS] = ok ? qg - dg0 : 0u;
                     c_a[CS] = aa[S2];
-#if KS_OPT
                     c_s[CS] = as_[S2];
-#endif
                     lq = ok ? qg - dg0 : p;
                     if constexpr (REC) {
                         /* q1's own old entry: block t-2 or t-3 in O, else Q */
@@ -445,11 +429,7 @@ __global__ __launch_bounds__(KS_THR) void lzf_cand_stream_kernel(LzfBatch bt, ui
                 const KsWin &d = pw[PS];
                 const uint32_t p = d.lb + lane;
                 const bool act = d.live && p < d.n - 2u;
-#if KS_OPT
                 const uint2 pb = d.lb + 64u + 8u <= d.n ? pa[PS] : ks_fix(pa[PS], d.n, p);
-#else
-                const uint2 pb = ks_fix(pa[PS], d.n, p);
-#endif
                 const uint32_t sl = dv_slot(pb.x);
                 if constexpr (REC) {
                     /* the stream position of this lane is the block's (the
@@ -466,17 +446,12 @@ __global__ __launch_bounds__(KS_THR) void lzf_cand_stream_kernel(LzfBatch bt, ui
                     *(uint4 *)&D[PS][j][4] = make_uint4(d.lb, d.g0, d.live, 0u);
                 }
                 aa[PS] = pb;
-#if KS_OPT
                 as_[PS] = sl;
-#endif
             }
             KS_TM(5);
         }
         /* ---- the step's loads, every wave: the agreement bytes of C1, then
          * the window of block t + KS_PF --------------------------------------- */
-#ifdef KS_ABL_LD     /* diagnostics: the agreement load at p's own line (outputs wrong) */
-        lq = pw[PS].lb + lane;
-#endif
         c_b[CS] = ks_ld(lsrc, ln, lq);
         if constexpr (REC) c_b2[CS] = ks_ld(lsrc, ln, lq2);
         pw[PS] = window_or_none(KS_WINS * (t + KS_PF) + jj);
