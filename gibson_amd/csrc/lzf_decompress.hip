@@ -338,6 +338,115 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
     }
 }
 
+/* the pipe's input ring: the consumer reads round k's literals,
+ * [base_k, base_k + 161), while the producer stages for round k + 1: staging
+ * runs when fewer than 192 bytes are ahead of base and fills up to base + 320
+ * (16-byte aligned), so it overwrites only bytes before
+ * base_{k+1} + 320 - 512 <= base_k - 32 (base_{k+1} <= base_k + 160) */
+#define CD_IN_RINGP 512u
+/* CD_TOKOUT: the input ring's first 32 bytes are mirrored right after it */
+#define CD_IN_MIRROR 32u
+#ifndef CD_TOKOUT
+#define CD_TOKOUT 0
+#endif
+/* LDS store of exactly m (1..16) bytes of v at p (unaligned: gfx950's LDS
+ * takes unaligned b128/b64/b32/b16 accesses) */
+__device__ __forceinline__ void cd_st(uint8_t *p, uint4 v, uint32_t m)
+{
+    if (m >= 16u) {
+        __builtin_memcpy(p, &v, 16);
+        return;
+    }
+    uint32_t a = v.x, b = v.y, c = v.z, d = v.w;
+    if (m & 8u) {
+        const uint2 t = make_uint2(a, b);
+        __builtin_memcpy(p, &t, 8);
+        p += 8;
+        a = c;
+        b = d;
+    }
+    if (m & 4u) {
+        __builtin_memcpy(p, &a, 4);
+        p += 4;
+        a = b;
+    }
+    if (m & 2u) {
+        const uint16_t t = (uint16_t)a;
+        __builtin_memcpy(p, &t, 2);
+        p += 2;
+        a >>= 16;
+    }
+    if (m & 1u) *p = (uint8_t)a;
+}
+
+__device__ __forceinline__ uint4 cd_ld(const uint8_t *p)
+{
+    uint4 v;
+    __builtin_memcpy(&v, p, 16);
+    return v;
+}
+
+/* Token-granular output of one round (CD_TOKOUT, rounds whose output stays
+ * inside the window: O + total <= ring, so positions are ring offsets and
+ * nothing wraps or is overwritten).  Lane l copies token l whole, 16 bytes
+ * per LDS access (src/lzf_d.c:86-91 literal, :133-142 back-reference):
+ *   - a literal from the input ring (its first 32 bytes are mirrored past
+ *     its end, so a token's bytes are contiguous);
+ *   - a back-reference from the window, 16 bytes at a time; one that overlaps
+ *     itself (distance d < 16 and d < length: the byte-serial copy replicates
+ *     the last d bytes) first writes one period multiple L = d * ceil(16 / d)
+ *     byte by byte, then copies 16 bytes at a time from L back.
+ * A token is copied in the first pass in which no token before it that is
+ * still pending can overlap its source: the nearest pending token before it
+ * ends at or before its source, or its source lies wholly before the round.
+ * The lowest pending token always qualifies, so every pass makes progress;
+ * passes follow the round's in-round reference chains. */
+__device__ __forceinline__ void cd_output_tok(uint8_t *inr, uint8_t *outr, uint8_t *dst, uint32_t O, uint32_t total,
+                                              uint32_t ntok, uint32_t w, uint32_t lane, uint32_t unit, uint32_t &F)
+{
+    const bool act = lane < ntok;
+    const uint32_t rel = w & 0xFFFFu, info = w >> 17;
+    const bool lit = (w >> 16) & 1u;
+    const uint32_t nrel = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane + 1u) & 63u) << 2), (int)rel);
+    const uint32_t len = act ? ((lane + 1u < ntok ? nrel : total) - rel) : 0u;
+    const uint32_t Ot = O + rel, end = Ot + len;
+    /* a back-reference's source [s, e): the bytes it reads that precede it */
+    const uint32_t s = lit ? 0u : Ot - info;
+    const uint32_t e = lit ? 0u : (s + len < Ot ? s + len : Ot);
+    bool done = !act;
+    for (;;) {
+        const uint64_t D = __ballot(done);
+        if (D == ~0ull) break;
+        const uint64_t before = ~D & ((1ull << lane) - 1ull);
+        const uint32_t js = before ? 63u - (uint32_t)__builtin_clzll(before) : 0u;
+        const uint32_t endj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(js << 2), (int)end);
+        const bool ready = !done && (lit || e <= O || before == 0ull || endj <= s);
+        if (ready) {
+            if (lit) {
+                const uint32_t ri = (Ot + info) & (CD_IN_RINGP - 1u);
+                for (uint32_t c = 0; c < len; c += 16u)
+                    cd_st(outr + Ot + c, cd_ld(inr + ri + c), len - c);
+            } else {
+                uint32_t d = info, c = 0u;
+                if (d < 16u && d < len) {
+                    const uint32_t L = d * ((15u + d) / d);
+                    const uint32_t pre = len < L ? len : L;
+                    for (; c < pre; c++) outr[Ot + c] = outr[Ot + c - d];
+                    d = L;
+                }
+                for (; c < len; c += 16u) cd_st(outr + Ot + c, cd_ld(outr + Ot + c - d), len - c);
+            }
+        }
+        cd_fence();
+        done = done || ready;
+    }
+    /* completed flush units to HBM, 16 bytes per lane */
+    while (O + total - F >= unit) {
+        if (16u * lane < unit) __builtin_memcpy(dst + F + 16u * lane, outr + F + 16u * lane, 16);
+        F += unit;
+    }
+}
+
 /* a value past the batch's stated max_out_cap is refused, never overrun */
 __device__ __forceinline__ bool cd_refused(const LzfBatch &bt, uint32_t v, uint32_t lane)
 {
@@ -404,12 +513,6 @@ struct CdSlot {
     uint32_t ntok, total, last;
     int32_t err;
 };
-/* the pipe's input ring: the consumer reads round k's literals,
- * [base_k, base_k + 161), while the producer stages for round k + 1: staging
- * runs when fewer than 192 bytes are ahead of base and fills up to base + 320
- * (16-byte aligned), so it overwrites only bytes before
- * base_{k+1} + 320 - 512 <= base_k - 32 (base_{k+1} <= base_k + 160) */
-#define CD_IN_RINGP 512u
 
 __device__ __forceinline__ void cd_stage_pipe(uint8_t *inr, const uint8_t *src, uint32_t base, uint32_t avail,
                                               uint32_t &loaded, uint32_t lane)
@@ -418,7 +521,11 @@ __device__ __forceinline__ void cd_stage_pipe(uint8_t *inr, const uint8_t *src, 
     if (loaded < need) {
         const uint32_t to = min(avail, (base + 320u) & ~15u);
         const uint32_t x = loaded + 16u * lane;       /* loaded is a multiple of 16 here */
-        if (x < to) *(uint4 *)(inr + (x & (CD_IN_RINGP - 1u))) = cd_ld16(src + x, to - x);
+        if (x < to) {
+            const uint4 v = cd_ld16(src + x, to - x);
+            *(uint4 *)(inr + (x & (CD_IN_RINGP - 1u))) = v;
+            if (CD_TOKOUT && (x & (CD_IN_RINGP - 1u)) < CD_IN_MIRROR) *(uint4 *)(inr + CD_IN_RINGP + (x & (CD_IN_RINGP - 1u))) = v;
+        }
         loaded = to;
         cd_fence();
     }
@@ -427,8 +534,8 @@ __device__ __forceinline__ void cd_stage_pipe(uint8_t *inr, const uint8_t *src, 
 __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, uint32_t out_ring)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t *inr = smem;                               /* CD_IN_RINGP */
-    CdSlot *slot = (CdSlot *)(smem + CD_IN_RINGP);     /* 2 */
+    uint8_t *inr = smem;                               /* CD_IN_RINGP (+ the mirror, CD_TOKOUT) */
+    CdSlot *slot = (CdSlot *)(smem + CD_IN_RINGP + (CD_TOKOUT ? CD_IN_MIRROR : 0u));   /* 2 */
     uint32_t *mark = (uint32_t *)(slot + 2);           /* the consumer's 64 token-start marks */
     uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* unused (was the removed walk's token starts) */
     uint8_t *sink = tokpos + CD_LANES;                 /* the consumer's idle-lane byte sink */
@@ -487,9 +594,13 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
             err = __builtin_amdgcn_readfirstlane(s.err);
             if (err) break;      /* the failing round writes nothing */
             const uint32_t w = s.tok[lane];
-            cd_output<CD_IN_RINGP>(smem, (uint32_t)(outr - smem), omask, mark, (uint32_t)(sink - smem), dst, O,
-                                   total, lane < ntok, O + (w & 0xFFFFu), (w >> 17) | ((w & 0x10000u) << 15), lane,
-                                   F);
+            if (CD_TOKOUT && O + total <= omask + 1u)
+                cd_output_tok(inr, outr, dst, O, total, ntok, w, lane,
+                              (omask + 1u) / 2u < 1024u ? (omask + 1u) / 2u : 1024u, F);
+            else
+                cd_output<CD_IN_RINGP>(smem, (uint32_t)(outr - smem), omask, mark, (uint32_t)(sink - smem), dst, O,
+                                       total, lane < ntok, O + (w & 0xFFFFu), (w >> 17) | ((w & 0x10000u) << 15),
+                                       lane, F);
             O += total;
             if (last) break;
             cd_barrier(tw);
@@ -524,7 +635,10 @@ hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s)
     while (ring < b.max_len && ring < CD_OUT_MAX) ring <<= 1;
     hipError_t e;
     if (CD_PIPE && ring >= CD_PIPE_MIN_RING) {
-        const size_t lds = CD_IN_RINGP + 2u * sizeof(CdSlot) + 5u * CD_LANES + 16u + ring;
+        /* CD_TOKOUT: + the input ring's mirror and 16 bytes past the window
+         * (a 16-byte read near its end) */
+        const size_t lds = CD_IN_RINGP + 2u * sizeof(CdSlot) + 5u * CD_LANES + 16u + ring +
+                           (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u);
         e = hipFuncSetAttribute((const void *)lzf_decompress_pipe_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

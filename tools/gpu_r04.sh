@@ -36,6 +36,11 @@ for st in "$@"; do
     pmcmix) for c in FETCH_SIZE WRITE_SIZE; do
               timeout -s KILL 600 rocprofv3 --pmc $c --output-format csv -d $O/pmc_mixed_$c -o run -- python3 bench.py --workload mixed16k --total 4194304 --steps 1 --warmup 0 --no-cpu > $O/pmc_mixed_$c.log 2>&1 || exit 1
               tail -1 $O/pmc_mixed_$c.log | cut -c1-200; done ;;
+    dab:*)  # dab:<kind>:<n>:<count>:<variant>[:<variant>] -- decode A/B (AB_MODE=decompress), base vs variants
+            IFS=: read -r _ k nn c rest <<< "$st"; libs="gibson_amd/liblzf_hip.so"; for x in ${rest//:/ }; do libs="$libs gibson_amd/liblzf_hip_$x.so"; done
+            AB_MODE=decompress AB_SEED=$([ $k = 0 ] && echo 0x5EED0004 || ([ $k = 2 ] && echo 0x5EED0003 || ([ $k = 3 ] && echo 0x5EED0005 || echo 0x5EED0002))) \
+              timeout -k 10 600 python -u tools/ab_compress.py $k $nn $c 5 $libs > $O/dab_${k}_${nn}_${rest//:/_}.txt 2>&1 || exit 1
+            grep -v amdgpu.ids $O/dab_${k}_${nn}_${rest//:/_}.txt ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
