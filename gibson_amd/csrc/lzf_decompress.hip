@@ -439,7 +439,16 @@ __device__ __forceinline__ void cd_output_tok(uint8_t *inr, uint8_t *outr, uint8
         }
         cd_fence();
         done = done || ready;
+#ifdef CD_TIMING
+        if (lane == 0u) atomicAdd(&cd_tstat[4], 1ull);      /* passes */
+#endif
     }
+#ifdef CD_TIMING
+    if (lane == 0u) {
+        atomicAdd(&cd_tstat[5], 1ull);                       /* rounds in token mode */
+        atomicAdd(&cd_tstat[6], (unsigned long long)ntok);   /* their tokens */
+    }
+#endif
     /* completed flush units to HBM, 16 bytes per lane */
     while (O + total - F >= unit) {
         if (16u * lane < unit) __builtin_memcpy(dst + F + 16u * lane, outr + F + 16u * lane, 16);

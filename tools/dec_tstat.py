@@ -47,6 +47,8 @@ def main():
         names = ["prod busy", "prod wait", "cons busy", "cons wait"]
         print(os.path.basename(path), " ".join(f"{nm} {st[i] / rounds:8.0f}" for i, nm in enumerate(names)),
               "cycles per ~round")
+        if st[5]:   # the token-granular output stage (CD_TOKOUT): passes per token-mode round
+            print(f"  token mode: {st[5]} rounds, {st[4] / st[5]:.2f} passes and {st[6] / st[5]:.1f} tokens per round")
 
 
 if __name__ == "__main__":

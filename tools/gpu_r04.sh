@@ -41,6 +41,10 @@ for st in "$@"; do
             AB_MODE=decompress AB_SEED=$([ $k = 0 ] && echo 0x5EED0004 || ([ $k = 2 ] && echo 0x5EED0003 || ([ $k = 3 ] && echo 0x5EED0005 || echo 0x5EED0002))) \
               timeout -k 10 600 python -u tools/ab_compress.py $k $nn $c 5 $libs > $O/dab_${k}_${nn}_${rest//:/_}.txt 2>&1 || exit 1
             grep -v amdgpu.ids $O/dab_${k}_${nn}_${rest//:/_}.txt ;;
+    tokstat) timeout -k 10 300 python -u tools/dec_tstat.py 0 8192 1048576 gibson_amd/liblzf_hip_time.so gibson_amd/liblzf_hip_toktime.so > $O/tokstat.txt 2>&1 || exit 1
+            grep -v amdgpu.ids $O/tokstat.txt ;;
+    pmctok) timeout -k 10 600 bash tools/pmc_dec_ab.sh "" tok > $O/pmctok.txt 2>&1 || exit 1
+            cat $O/pmctok.txt; cp gpurun_out/mix_*.txt $O/ ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
