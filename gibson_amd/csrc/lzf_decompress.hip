@@ -157,11 +157,22 @@ __device__ __forceinline__ void cd_stage(uint8_t *inr, const uint8_t *src, uint3
 
 /* step 1: lane l gets the round-relative start of token l (CD_ROUND: none);
  * nbase = the input offset after the round's last token */
+/* MIR: the ring's first bytes are mirrored past its end (the pipe), so a
+ * token's bytes come in one unaligned LDS read */
+template <bool MIR = false>
 __device__ __forceinline__ uint32_t cd_discover(const uint8_t *inr, uint32_t imask, uint8_t *tokpos,
                                                 uint32_t base, uint32_t in_len, uint32_t lane, uint32_t &nbase)
 {
     const uint32_t pa = 2u * lane, pb = pa + 1u;
-    const uint32_t ca = inr[(base + pa) & imask], cb = inr[(base + pb) & imask];
+    uint32_t ca, cb;
+    if (MIR) {
+        const uint32_t h = *(const uint16_t *)(inr + ((base + pa) & imask));
+        ca = h & 0xFFu;
+        cb = h >> 8;
+    } else {
+        ca = inr[(base + pa) & imask];
+        cb = inr[(base + pb) & imask];
+    }
     const uint32_t ta = cd_tsz(ca), tb = cd_tsz(cb);
     (void)tokpos;
     /* jump tables J0..J5 over the round's 128 positions packed two per lane
@@ -208,15 +219,26 @@ __device__ __forceinline__ uint32_t cd_discover(const uint8_t *inr, uint32_t ima
 struct CdRound {
     uint32_t rel, tinfo, total;
     int32_t err;
+    bool overlap;            /* a back-reference of the round overlaps itself (distance < length) */
 };
 
+template <bool MIR = false>
 __device__ __forceinline__ CdRound cd_decode(const uint8_t *inr, uint32_t imask, uint32_t base, uint32_t x,
                                              uint32_t O, uint32_t in_len, uint32_t cap)
 {
     const bool tok = x < CD_ROUND;
     const uint32_t ip = base + (tok ? x : 0u);
-    const uint32_t c = inr[ip & imask];
-    const uint32_t b1 = inr[(ip + 1u) & imask], b2 = inr[(ip + 2u) & imask];
+    uint32_t c, b1, b2;
+    if (MIR) {
+        const uint32_t w = *(const uint32_t *)(inr + (ip & imask));
+        c = w & 0xFFu;
+        b1 = (w >> 8) & 0xFFu;
+        b2 = (w >> 16) & 0xFFu;
+    } else {
+        c = inr[ip & imask];
+        b1 = inr[(ip + 1u) & imask];
+        b2 = inr[(ip + 2u) & imask];
+    }
     const bool lit = c < 32u;
     const bool l7 = (c >> 5) == 7u;                     /* length in the next byte */
     const uint32_t back = ((c & 31u) << 8) + (l7 ? b2 : b1) + 1u;   /* back-refs only */
@@ -248,6 +270,7 @@ __device__ __forceinline__ CdRound cd_decode(const uint8_t *inr, uint32_t imask,
     }
     const uint64_t EB = __ballot(e != 0);
     r.err = EB ? (int32_t)cd_rl((uint32_t)e, (uint32_t)__builtin_ctzll(EB)) : 0;
+    r.overlap = __ballot(tok && !lit && back < olen) != 0ull;
     return r;
 }
 
@@ -285,10 +308,20 @@ __device__ __forceinline__ void cd_flush(const uint8_t *lds, uint32_t outr_off, 
  * resolved source resolves it, a pending one doubles the pointer).  Idle
  * lanes store their byte to a sink slot; every group goes to HBM as it
  * completes */
+/* CD_PERIOD: in a round whose producer flagged a self-overlapping
+ * back-reference (distance d < length, a run: src/lzf_d.c:137-142 copies
+ * byte-serially, so its bytes repeat with period d), a byte at offset x >= d
+ * of such a token takes its source in the token's first period,
+ * Ot - d + (x mod d), which lies before the token: a run that started in an
+ * earlier group resolves in one read instead of log2(64) doubling steps */
+#ifndef CD_PERIOD
+#define CD_PERIOD 1
+#endif
 template <uint32_t IN_RING>
 __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint32_t omask, uint32_t *mark,
                                              uint32_t sink_off, uint8_t *dst, uint32_t O, uint32_t total, bool tok,
-                                             uint32_t Ot, uint32_t tinfo, uint32_t lane, uint32_t &F)
+                                             uint32_t Ot, uint32_t tinfo, uint32_t lane, uint32_t &F,
+                                             bool per = false)
 {
     /* a flush unit of the window's completed bytes goes out as soon
      * as it is complete (half the window at most, so no byte is overwritten
@@ -312,7 +345,19 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
         const uint32_t tInf = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)tinfo);
         const uint32_t o = gb + lane;
         const uint32_t lit = (uint32_t)((int32_t)tInf >> 31);
-        const uint32_t so = o - tInf;
+        uint32_t so = o - tInf;
+        if (CD_PERIOD && per) {                        /* uniform: the producer's flag */
+            const uint32_t ot = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)Ot);
+            const uint32_t x = o - ot;
+            if (!lit && x >= tInf) {
+                /* x mod d: a float quotient, off by at most one, corrected */
+                const uint32_t qf = (uint32_t)((float)x * __builtin_amdgcn_rcpf((float)tInf));
+                int32_t r = (int32_t)(x - qf * tInf);
+                r = r < 0 ? r + (int32_t)tInf : r;
+                r = r >= (int32_t)tInf ? r - (int32_t)tInf : r;
+                so = ot - tInf + (uint32_t)r;
+            }
+        }
         const uint32_t a = (((o + tInf) & imask) & lit) | ((outr_off + (so & omask)) & ~lit);
         const uint32_t q = so - gb;
         const uint32_t b = lds[a];
@@ -344,7 +389,10 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
  * (16-byte aligned), so it overwrites only bytes before
  * base_{k+1} + 320 - 512 <= base_k - 32 (base_{k+1} <= base_k + 160) */
 #define CD_IN_RINGP 512u
-/* CD_TOKOUT: the input ring's first 32 bytes are mirrored right after it */
+/* CD_TOKOUT / CD_MIR: the input ring's first 32 bytes are mirrored right after it */
+#ifndef CD_MIR
+#define CD_MIR 1
+#endif
 #define CD_IN_MIRROR 32u
 #ifndef CD_TOKOUT
 #define CD_TOKOUT 0
@@ -533,7 +581,7 @@ __device__ __forceinline__ void cd_stage_pipe(uint8_t *inr, const uint8_t *src, 
         if (x < to) {
             const uint4 v = cd_ld16(src + x, to - x);
             *(uint4 *)(inr + (x & (CD_IN_RINGP - 1u))) = v;
-            if (CD_TOKOUT && (x & (CD_IN_RINGP - 1u)) < CD_IN_MIRROR) *(uint4 *)(inr + CD_IN_RINGP + (x & (CD_IN_RINGP - 1u))) = v;
+            if ((CD_TOKOUT || CD_MIR) && (x & (CD_IN_RINGP - 1u)) < CD_IN_MIRROR) *(uint4 *)(inr + CD_IN_RINGP + (x & (CD_IN_RINGP - 1u))) = v;
         }
         loaded = to;
         cd_fence();
@@ -543,8 +591,8 @@ __device__ __forceinline__ void cd_stage_pipe(uint8_t *inr, const uint8_t *src, 
 __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, uint32_t out_ring)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t *inr = smem;                               /* CD_IN_RINGP (+ the mirror, CD_TOKOUT) */
-    CdSlot *slot = (CdSlot *)(smem + CD_IN_RINGP + (CD_TOKOUT ? CD_IN_MIRROR : 0u));   /* 2 */
+    uint8_t *inr = smem;                               /* CD_IN_RINGP + the mirror */
+    CdSlot *slot = (CdSlot *)(smem + CD_IN_RINGP + (CD_TOKOUT || CD_MIR ? CD_IN_MIRROR : 0u));   /* 2 */
     uint32_t *mark = (uint32_t *)(slot + 2);           /* the consumer's 64 token-start marks */
     uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* unused (was the removed walk's token starts) */
     uint8_t *sink = tokpos + CD_LANES;                 /* the consumer's idle-lane byte sink */
@@ -571,8 +619,8 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
         for (uint32_t k = 0;; k++) {
             cd_stage_pipe(inr, src, base, avail, loaded, lane);
             uint32_t nbase;
-            const uint32_t x = cd_discover(inr, imask, tokpos, base, in_len, lane, nbase);
-            const CdRound r = cd_decode(inr, imask, base, x, O, in_len, cap);
+            const uint32_t x = cd_discover<CD_TOKOUT || CD_MIR>(inr, imask, tokpos, base, in_len, lane, nbase);
+            const CdRound r = cd_decode<CD_TOKOUT || CD_MIR>(inr, imask, base, x, O, in_len, cap);
             const uint32_t ntok = (uint32_t)__builtin_popcountll(__ballot(x < CD_ROUND));
             const uint32_t total = r.total;
             CdSlot &s = slot[k & 1u];
@@ -581,7 +629,7 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
             if (lane == 0) {
                 s.ntok = ntok;
                 s.total = total;
-                s.last = last;
+                s.last = (last ? 1u : 0u) | (r.overlap ? 2u : 0u);
                 s.err = r.err;
             }
             O += total;
@@ -598,7 +646,9 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
         for (uint32_t k = 0;; k++) {
             const CdSlot &s = slot[k & 1u];
             const uint32_t total = __builtin_amdgcn_readfirstlane(s.total);
-            const uint32_t last = __builtin_amdgcn_readfirstlane(s.last);
+            const uint32_t lastw = __builtin_amdgcn_readfirstlane(s.last);
+            const uint32_t last = lastw & 1u;
+            const bool per = (lastw & 2u) != 0u;
             const uint32_t ntok = __builtin_amdgcn_readfirstlane(s.ntok);
             err = __builtin_amdgcn_readfirstlane(s.err);
             if (err) break;      /* the failing round writes nothing */
@@ -609,7 +659,7 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
             else
                 cd_output<CD_IN_RINGP>(smem, (uint32_t)(outr - smem), omask, mark, (uint32_t)(sink - smem), dst, O,
                                        total, lane < ntok, O + (w & 0xFFFFu), (w >> 17) | ((w & 0x10000u) << 15),
-                                       lane, F);
+                                       lane, F, per);
             O += total;
             if (last) break;
             cd_barrier(tw);
@@ -644,10 +694,10 @@ hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s)
     while (ring < b.max_len && ring < CD_OUT_MAX) ring <<= 1;
     hipError_t e;
     if (CD_PIPE && ring >= CD_PIPE_MIN_RING) {
-        /* CD_TOKOUT: + the input ring's mirror and 16 bytes past the window
+        /* + the input ring's mirror; CD_TOKOUT: + 16 bytes past the window
          * (a 16-byte read near its end) */
         const size_t lds = CD_IN_RINGP + 2u * sizeof(CdSlot) + 5u * CD_LANES + 16u + ring +
-                           (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u);
+                           (CD_TOKOUT || CD_MIR ? CD_IN_MIRROR : 0u) + (CD_TOKOUT ? 16u : 0u);
         e = hipFuncSetAttribute((const void *)lzf_decompress_pipe_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

@@ -657,3 +657,23 @@ def test_host_batch_api(oracle):
     ok = olen > 0
     gibson_amd.host_decompress_batch(out, off[ok], olen[ok], dec, off[ok], ln[ok], dl, er)
     assert (dl[:ok.sum()] == 4096).all() and (er[:ok.sum()] == 0).all()
+
+
+def test_decode_self_overlapping_references(oracle):
+    # runs of every period 1..70 (a back-reference whose distance is below its
+    # length repeats its last d bytes, src/lzf_d.c:137-142), starting at
+    # every phase of a 64-byte output group, inside values past 4 KiB so the
+    # two-wave decoder (and its periodic-source path, CD_PERIOD) decodes them
+    from tests.gpu_batch import gpu_decompress
+    rnd = random.Random(70)
+    vals = []
+    for period in range(1, 71):
+        for phase in (0, 1, 17, 63):
+            pat = bytes(rnd.randrange(256) for _ in range(period))
+            head = bytes(rnd.randrange(256) for _ in range(4096 + phase))
+            body = (pat * (20000 // period + 2))[:rnd.randint(300, 12000)]
+            tail = synth(0, 0x5EED0DD0, period * 4 + phase, rnd.randint(100, 3000))
+            vals.append(head + body + tail)
+    streams = [oracle.compress(v, len(v) + len(v) // 16 + 64) for v in vals]
+    assert all(streams)
+    assert gpu_decompress(streams, [len(v) for v in vals]) == [(v, 0) for v in vals]

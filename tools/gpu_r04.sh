@@ -45,6 +45,11 @@ for st in "$@"; do
             grep -v amdgpu.ids $O/tokstat.txt ;;
     pmctok) timeout -k 10 600 bash tools/pmc_dec_ab.sh "" tok > $O/pmctok.txt 2>&1 || exit 1
             cat $O/pmctok.txt; cp gpurun_out/mix_*.txt $O/ ;;
+    abk:*)  # abk:<kind>:<n>:<count>:<variant>[:<variant>] -- compress A/B, product vs variants
+            IFS=: read -r _ k nn c rest <<< "$st"; libs="gibson_amd/liblzf_hip.so"; for x in ${rest//:/ }; do libs="$libs gibson_amd/liblzf_hip_$x.so"; done
+            AB_SEED=$([ $k = 0 ] && echo 0x5EED0004 || ([ $k = 2 ] && echo 0x5EED0003 || ([ $k = 3 ] && echo 0x5EED0005 || echo 0x5EED0002))) \
+              timeout -k 10 600 python -u tools/ab_compress.py $k $nn $c 3 $libs > $O/abk_${k}_${nn}_${rest//:/_}.txt 2>&1 || exit 1
+            grep -v amdgpu.ids $O/abk_${k}_${nn}_${rest//:/_}.txt ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
