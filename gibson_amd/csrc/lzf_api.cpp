@@ -193,7 +193,7 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s, ScratchUser who)
 #else
     const size_t per = table ? lzf_table_scratch_per_value(b.max_len) : lzf_lane_scratch_per_value(b.max_len);
 #endif
-    size_t want = per * (size_t)b.count + 1024;    /* + alignment and the parse's work counter */
+    size_t want = per * (size_t)b.count + 512;
     const size_t lim = scratch_limit(S.cap);
     if (want > lim) want = lim;
     if (want < 2 * per + 1024) want = 2 * per + 1024;     /* two pipeline halves */

@@ -157,22 +157,11 @@ __device__ __forceinline__ void cd_stage(uint8_t *inr, const uint8_t *src, uint3
 
 /* step 1: lane l gets the round-relative start of token l (CD_ROUND: none);
  * nbase = the input offset after the round's last token */
-/* MIR: the ring's first bytes are mirrored past its end (the pipe), so a
- * token's bytes come in one unaligned LDS read */
-template <bool MIR = false>
 __device__ __forceinline__ uint32_t cd_discover(const uint8_t *inr, uint32_t imask, uint8_t *tokpos,
                                                 uint32_t base, uint32_t in_len, uint32_t lane, uint32_t &nbase)
 {
     const uint32_t pa = 2u * lane, pb = pa + 1u;
-    uint32_t ca, cb;
-    if (MIR) {
-        const uint32_t h = *(const uint16_t *)(inr + ((base + pa) & imask));
-        ca = h & 0xFFu;
-        cb = h >> 8;
-    } else {
-        ca = inr[(base + pa) & imask];
-        cb = inr[(base + pb) & imask];
-    }
+    const uint32_t ca = inr[(base + pa) & imask], cb = inr[(base + pb) & imask];
     const uint32_t ta = cd_tsz(ca), tb = cd_tsz(cb);
     (void)tokpos;
     /* jump tables J0..J5 over the round's 128 positions packed two per lane
@@ -216,29 +205,22 @@ __device__ __forceinline__ uint32_t cd_discover(const uint8_t *inr, uint32_t ima
  * the owner info of its output bytes (tinfo: literal -> input ring index
  * o + tinfo, flagged in bit 31; back-ref -> distance), the round's output
  * bytes, and errno of the first failing token (0: none) */
+#ifndef CD_PER_RATIO
+#define CD_PER_RATIO 4u
+#endif
 struct CdRound {
     uint32_t rel, tinfo, total;
     int32_t err;
-    bool overlap;            /* a back-reference of the round overlaps itself (distance < length) */
+    bool overlap;            /* a back-reference of the round repeats its distance CD_PER_RATIO times */
 };
 
-template <bool MIR = false>
 __device__ __forceinline__ CdRound cd_decode(const uint8_t *inr, uint32_t imask, uint32_t base, uint32_t x,
                                              uint32_t O, uint32_t in_len, uint32_t cap)
 {
     const bool tok = x < CD_ROUND;
     const uint32_t ip = base + (tok ? x : 0u);
-    uint32_t c, b1, b2;
-    if (MIR) {
-        const uint32_t w = *(const uint32_t *)(inr + (ip & imask));
-        c = w & 0xFFu;
-        b1 = (w >> 8) & 0xFFu;
-        b2 = (w >> 16) & 0xFFu;
-    } else {
-        c = inr[ip & imask];
-        b1 = inr[(ip + 1u) & imask];
-        b2 = inr[(ip + 2u) & imask];
-    }
+    const uint32_t c = inr[ip & imask];
+    const uint32_t b1 = inr[(ip + 1u) & imask], b2 = inr[(ip + 2u) & imask];
     const bool lit = c < 32u;
     const bool l7 = (c >> 5) == 7u;                     /* length in the next byte */
     const uint32_t back = ((c & 31u) << 8) + (l7 ? b2 : b1) + 1u;   /* back-refs only */
@@ -270,7 +252,9 @@ __device__ __forceinline__ CdRound cd_decode(const uint8_t *inr, uint32_t imask,
     }
     const uint64_t EB = __ballot(e != 0);
     r.err = EB ? (int32_t)cd_rl((uint32_t)e, (uint32_t)__builtin_ctzll(EB)) : 0;
-    r.overlap = __ballot(tok && !lit && back < olen) != 0ull;
+    /* a run long enough that the shortcut saves doubling steps (CD_PER_RATIO
+     * periods or more) */
+    r.overlap = __ballot(tok && !lit && olen >= CD_PER_RATIO * back) != 0ull;
     return r;
 }
 
@@ -317,11 +301,10 @@ __device__ __forceinline__ void cd_flush(const uint8_t *lds, uint32_t outr_off, 
 #ifndef CD_PERIOD
 #define CD_PERIOD 1
 #endif
-template <uint32_t IN_RING>
+template <uint32_t IN_RING, bool PER = false>
 __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint32_t omask, uint32_t *mark,
                                              uint32_t sink_off, uint8_t *dst, uint32_t O, uint32_t total, bool tok,
-                                             uint32_t Ot, uint32_t tinfo, uint32_t lane, uint32_t &F,
-                                             bool per = false)
+                                             uint32_t Ot, uint32_t tinfo, uint32_t lane, uint32_t &F)
 {
     /* a flush unit of the window's completed bytes goes out as soon
      * as it is complete (half the window at most, so no byte is overwritten
@@ -346,7 +329,7 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
         const uint32_t o = gb + lane;
         const uint32_t lit = (uint32_t)((int32_t)tInf >> 31);
         uint32_t so = o - tInf;
-        if (CD_PERIOD && per) {                        /* uniform: the producer's flag */
+        if (PER) {                                     /* a round the producer flagged */
             const uint32_t ot = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)Ot);
             const uint32_t x = o - ot;
             if (!lit && x >= tInf) {
@@ -389,10 +372,10 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
  * (16-byte aligned), so it overwrites only bytes before
  * base_{k+1} + 320 - 512 <= base_k - 32 (base_{k+1} <= base_k + 160) */
 #define CD_IN_RINGP 512u
-/* CD_TOKOUT / CD_MIR: the input ring's first 32 bytes are mirrored right after it */
-#ifndef CD_MIR
-#define CD_MIR 1
-#endif
+/* CD_TOKOUT: the input ring's first 32 bytes are mirrored right after it
+ * (also tried for single unaligned reads of a token's bytes in steps 1-2:
+ * slower, 11.14 -> 11.85 ms mixed16k, 21.75 -> 24.00 Zipf, 17.33 -> 18.88
+ * text64k, profiles/r04/dab_*_noper_nomir.txt) */
 #define CD_IN_MIRROR 32u
 #ifndef CD_TOKOUT
 #define CD_TOKOUT 0
@@ -581,7 +564,7 @@ __device__ __forceinline__ void cd_stage_pipe(uint8_t *inr, const uint8_t *src, 
         if (x < to) {
             const uint4 v = cd_ld16(src + x, to - x);
             *(uint4 *)(inr + (x & (CD_IN_RINGP - 1u))) = v;
-            if ((CD_TOKOUT || CD_MIR) && (x & (CD_IN_RINGP - 1u)) < CD_IN_MIRROR) *(uint4 *)(inr + CD_IN_RINGP + (x & (CD_IN_RINGP - 1u))) = v;
+            if (CD_TOKOUT && (x & (CD_IN_RINGP - 1u)) < CD_IN_MIRROR) *(uint4 *)(inr + CD_IN_RINGP + (x & (CD_IN_RINGP - 1u))) = v;
         }
         loaded = to;
         cd_fence();
@@ -591,8 +574,8 @@ __device__ __forceinline__ void cd_stage_pipe(uint8_t *inr, const uint8_t *src, 
 __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, uint32_t out_ring)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t *inr = smem;                               /* CD_IN_RINGP + the mirror */
-    CdSlot *slot = (CdSlot *)(smem + CD_IN_RINGP + (CD_TOKOUT || CD_MIR ? CD_IN_MIRROR : 0u));   /* 2 */
+    uint8_t *inr = smem;                               /* CD_IN_RINGP (+ the mirror, CD_TOKOUT) */
+    CdSlot *slot = (CdSlot *)(smem + CD_IN_RINGP + (CD_TOKOUT ? CD_IN_MIRROR : 0u));   /* 2 */
     uint32_t *mark = (uint32_t *)(slot + 2);           /* the consumer's 64 token-start marks */
     uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* unused (was the removed walk's token starts) */
     uint8_t *sink = tokpos + CD_LANES;                 /* the consumer's idle-lane byte sink */
@@ -619,8 +602,8 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
         for (uint32_t k = 0;; k++) {
             cd_stage_pipe(inr, src, base, avail, loaded, lane);
             uint32_t nbase;
-            const uint32_t x = cd_discover<CD_TOKOUT || CD_MIR>(inr, imask, tokpos, base, in_len, lane, nbase);
-            const CdRound r = cd_decode<CD_TOKOUT || CD_MIR>(inr, imask, base, x, O, in_len, cap);
+            const uint32_t x = cd_discover(inr, imask, tokpos, base, in_len, lane, nbase);
+            const CdRound r = cd_decode(inr, imask, base, x, O, in_len, cap);
             const uint32_t ntok = (uint32_t)__builtin_popcountll(__ballot(x < CD_ROUND));
             const uint32_t total = r.total;
             CdSlot &s = slot[k & 1u];
@@ -656,10 +639,14 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
             if (CD_TOKOUT && O + total <= omask + 1u)
                 cd_output_tok(inr, outr, dst, O, total, ntok, w, lane,
                               (omask + 1u) / 2u < 1024u ? (omask + 1u) / 2u : 1024u, F);
+            else if (CD_PERIOD && per)   /* its own copy of the loop: the other rounds run the plain one */
+                cd_output<CD_IN_RINGP, true>(smem, (uint32_t)(outr - smem), omask, mark, (uint32_t)(sink - smem), dst,
+                                             O, total, lane < ntok, O + (w & 0xFFFFu),
+                                             (w >> 17) | ((w & 0x10000u) << 15), lane, F);
             else
                 cd_output<CD_IN_RINGP>(smem, (uint32_t)(outr - smem), omask, mark, (uint32_t)(sink - smem), dst, O,
                                        total, lane < ntok, O + (w & 0xFFFFu), (w >> 17) | ((w & 0x10000u) << 15),
-                                       lane, F, per);
+                                       lane, F);
             O += total;
             if (last) break;
             cd_barrier(tw);
@@ -694,10 +681,10 @@ hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s)
     while (ring < b.max_len && ring < CD_OUT_MAX) ring <<= 1;
     hipError_t e;
     if (CD_PIPE && ring >= CD_PIPE_MIN_RING) {
-        /* + the input ring's mirror; CD_TOKOUT: + 16 bytes past the window
+        /* CD_TOKOUT: + the input ring's mirror and 16 bytes past the window
          * (a 16-byte read near its end) */
         const size_t lds = CD_IN_RINGP + 2u * sizeof(CdSlot) + 5u * CD_LANES + 16u + ring +
-                           (CD_TOKOUT || CD_MIR ? CD_IN_MIRROR : 0u) + (CD_TOKOUT ? 16u : 0u);
+                           (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u);
         e = hipFuncSetAttribute((const void *)lzf_decompress_pipe_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

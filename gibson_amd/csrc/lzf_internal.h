@@ -61,7 +61,6 @@ struct LzfLaneScratch {
     uint64_t cstride;
     uint64_t bstride;
     uint32_t force_fix;    /* diagnostics: take the atomic-order repair path */
-    uint32_t *work;        /* the persistent parse's value counter (zeroed before each launch) */
 };
 
 /* compress scratch of the table generation (lzf_cand.hip), device pointers:

@@ -934,41 +934,26 @@ extern "C" int lzf_gpu_debug_sites(unsigned long long *out16, int reset)
 #ifndef K2_LITX
 #define K2_LITX 3u       /* free literals taken after a literal in the same iteration (0: none) */
 #endif
+enum { K2_STEP = 0, K2_RESOLVE = 1, K2_DECIDE = 2, K2_EXTEND = 3, K2_EMIT = 4, K2_DONE = 5 };
 
-/* K2_PERSIST = 1: persistent lanes.  The grid holds only the lanes that stay
- * resident, and a lane that finishes its value takes the next one from a
- * counter in the scratch (one atomic per wave per hand-out), so a wave no
- * longer waits for its slowest value while its other lanes idle.  On mixed
- * data the slowest of a wave's 64 values takes 1.37x their mean iterations
- * (tools/wave_balance.c). */
-#ifndef K2_PERSIST
-#define K2_PERSIST 1
-#endif
-#ifndef K2_BATCHK
-#define K2_BATCHK 16u       /* finished lanes of a wave that wait to be finalized together */
-#endif
-enum { K2_STEP = 0, K2_RESOLVE = 1, K2_DECIDE = 2, K2_EXTEND = 3, K2_EMIT = 4, K2_DONE = 5, K2_NEXT = 6,
-       K2_EXIT = 7 };
-
-#ifdef K2_WPE          /* diagnostic: waves per SIMD the compiler must fit */
-#define K2_ATTR __attribute__((amdgpu_waves_per_eu(K2_WPE, K2_WPE)))
-#else
-#define K2_ATTR
-#endif
-__global__ __launch_bounds__(K2_THREADS) K2_ATTR void lzf_parse_lane_kernel(LzfBatch bt, LzfLaneScratch sc)
+__global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt, LzfLaneScratch sc)
 {
-    /* the value of this lane and where it lives (set per value) */
-    uint32_t v = 0u, n = 0u, cap = 0u;
-    const uint8_t *src = nullptr;
-    uint8_t *dst = nullptr;
-    const uint16_t *cand = nullptr;
-    uint32_t *bits = nullptr;
+    const uint32_t v = blockIdx.x * K2_THREADS + threadIdx.x;
+    if (v >= bt.count) return;
+    const uint32_t n = bt.in_len[v], cap = bt.out_cap[v];
+    /* src/lzf_c.c:131; past the stated max_len (the scratch stride): refused */
+    if (n == 0u || cap == 0u || n > bt.max_len) { bt.out_len[v] = 0u; return; }
+    const uint8_t *src = bt.in + bt.in_off[v];
+    uint8_t *dst = bt.out + bt.out_off[v];
+    const uint16_t *cand = sc.cand + (uint64_t)v * sc.cstride;
+    uint32_t *bits = sc.bits + (uint64_t)v * sc.bstride;
+
     /* output: aligned dwords at da; acc holds the bytes from dword fw on */
-    uint32_t dm = 0u;
-    uint8_t *da = nullptr;
+    const uint32_t dm = (uint32_t)((uintptr_t)dst & 3u);
+    uint8_t *const da = dst - dm;
     uint64_t acc = 0;
-    uint32_t accn = 0u, fw = 0;
-    uint32_t hx = 0u;                   /* header byte of the open run (index from da) */
+    uint32_t accn = dm, fw = 0;
+    uint32_t hx = dm;                   /* header byte of the open run (index from da) */
     /* completed dwords [fs, fw) wait in pb0..2 and go out as one 16-byte
      * store: every store instruction of the wave touches 64 lines (one
      * per lane's value), so fewer, wider stores */
@@ -1003,13 +988,7 @@ __global__ __launch_bounds__(K2_THREADS) K2_ATTR void lzf_parse_lane_kernel(LzfB
     uint32_t ms = 0u, me = 0u;         /* the last match: [ms, me) */
     uint32_t rel = 0u, q = 0u, k = 0u, lim = 0u, m = 0u;
     bool ok = true;
-    uint32_t mode = K2_NEXT;
-    const uint32_t lane = threadIdx.x & 63u;
-#if K2_PERSIST
-    uint32_t *const work = sc.work;
-#endif
-    /* a lane's first value (non-persistent: its only one) */
-    [[maybe_unused]] bool first = true;
+    uint32_t mode = n >= 3u ? K2_STEP : K2_DONE;
 
 /* completed dwords [fs, fw) wait in pb0..2 (slot fw - fs) and leave with
  * the fourth as one 16-byte store; slot and patch selects instead of
@@ -1083,62 +1062,8 @@ __global__ __launch_bounds__(K2_THREADS) K2_ATTR void lzf_parse_lane_kernel(LzfB
         if (++run == LZF_MAX_LIT) { K2_PATCH(hx, LZF_MAX_LIT - 1u); run = 0u; o++; } \
     } while (0)
 
-    for (;;) {
-        /* ---- hand-out: lanes without a value take the next one ------------- */
-        const uint64_t want = __ballot(mode == K2_NEXT);
-        if (want) {
-#if K2_PERSIST
-            const uint32_t lead = (uint32_t)__builtin_ctzll(want);
-            uint32_t base = 0u;
-            if (lane == lead) base = atomicAdd(work, (uint32_t)__builtin_popcountll(want));
-            base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)lead);
-            const uint32_t nv = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
-                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
-#else
-            const uint32_t nv = first ? blockIdx.x * K2_THREADS + threadIdx.x : 0xFFFFFFFFu;
-#endif
-            if (mode == K2_NEXT) {
-                first = false;
-                v = nv;
-                if (v >= bt.count) {
-                    mode = K2_EXIT;
-                } else {
-                    n = bt.in_len[v];
-                    cap = bt.out_cap[v];
-                    src = bt.in + bt.in_off[v];
-                    dst = bt.out + bt.out_off[v];
-                    cand = sc.cand + (uint64_t)v * sc.cstride;
-                    bits = sc.bits + (uint64_t)v * sc.bstride;
-                    dm = (uint32_t)((uintptr_t)dst & 3u);
-                    da = dst - dm;
-                    acc = 0;
-                    accn = dm;
-                    fw = 0u;
-                    hx = dm;
-                    pb0 = pb1 = pb2 = fs = 0u;
-                    wb = 0xFFFFFFF0u;
-                    W = make_uint4(0, 0, 0, 0);
-                    o = 1u;
-                    run = 0u;
-                    p = 0u;
-                    cb = 0xFFFFFFE0u;
-                    cw = curw = fl = 0u;
-                    ms = me = 0u;
-                    rel = q = k = lim = m = 0u;
-                    ok = true;
-                    /* src/lzf_c.c:131; past the stated max_len (the scratch
-                     * stride): refused */
-                    if (n == 0u || cap == 0u || n > bt.max_len) {
-                        bt.out_len[v] = 0u;
-                        mode = K2_NEXT;
-                    } else {
-                        mode = n >= 3u ? K2_STEP : K2_DONE;
-                    }
-                }
-            }
-        }
-        if (!__ballot(mode != K2_EXIT)) break;
-        if (mode != K2_DONE && mode != K2_NEXT && mode != K2_EXIT) K2_SITE(0);
+    while (__ballot(mode != K2_DONE)) {
+        if (mode != K2_DONE) K2_SITE(0);
         /* ---- the cand word of p ------------------------------------------ */
         if (mode == K2_STEP) {                                            /* src/lzf_c.c:145 */
             if (p >= n - 2u) {
@@ -1344,36 +1269,24 @@ __global__ __launch_bounds__(K2_THREADS) K2_ATTR void lzf_parse_lane_kernel(LzfB
                 }
             }
         }
-        /* ---- the value's end: the tail and the last stores, for the wave's
-         * finished lanes together once K2_BATCHK of them (or all) wait, so the
-         * tail and hand-out code runs once per batch, not once per lane ------ */
-        const uint64_t fin = __ballot(mode == K2_DONE);
-        const bool go_fin = fin && ((uint32_t)__builtin_popcountll(fin) >= K2_BATCHK ||
-                                    !__ballot(mode != K2_DONE && mode != K2_NEXT && mode != K2_EXIT));
-        if (go_fin && mode == K2_DONE) {
-            if (!ok || o + 3u > cap) {                                   /* src/lzf_c.c:276 */
-                bt.out_len[v] = 0u;
-            } else {
-                while (p < n) {                                          /* src/lzf_c.c:279-288 */
-                    K2_LITERAL(p);
-                    p++;
-                }
-                if (run) K2_PATCH(hx, run - 1u);
-                else o--;
-                for (uint32_t i = fs; i < fw; i++) {
-                    const uint32_t wv = i == fs ? pb0 : i == fs + 1u ? pb1 : pb2;
-                    if (i == 0u && dm != 0u)
-                        for (uint32_t t = dm; t < 4u; t++) da[t] = (uint8_t)(wv >> (8u * t));
-                    else
-                        *(uint32_t *)(da + 4u * i) = wv;
-                }
-                for (uint32_t t = 0; t < accn; t++)
-                    if (4u * fw + t >= dm) da[4u * fw + t] = (uint8_t)(acc >> (8u * t));
-                bt.out_len[v] = o;
-            }
-            mode = K2_NEXT;
-        }
     }
+    if (!ok || o + 3u > cap) { bt.out_len[v] = 0u; return; }          /* src/lzf_c.c:276 */
+    while (p < n) {                                                   /* src/lzf_c.c:279-288 */
+        K2_LITERAL(p);
+        p++;
+    }
+    if (run) K2_PATCH(hx, run - 1u);
+    else o--;
+    for (uint32_t i = fs; i < fw; i++) {
+        const uint32_t wv = i == fs ? pb0 : i == fs + 1u ? pb1 : pb2;
+        if (i == 0u && dm != 0u)
+            for (uint32_t t = dm; t < 4u; t++) da[t] = (uint8_t)(wv >> (8u * t));
+        else
+            *(uint32_t *)(da + 4u * i) = wv;
+    }
+    for (uint32_t t = 0; t < accn; t++)
+        if (4u * fw + t >= dm) da[4u * fw + t] = (uint8_t)(acc >> (8u * t));
+    bt.out_len[v] = o;
 #undef K2_STORE16
 #undef K2_PUT
 #undef K2_PATCH
@@ -1758,9 +1671,7 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
     const size_t half = pipe ? (scratch_bytes / 2u) & ~(size_t)255 : scratch_bytes;
     uint64_t chunk = half / lzf_lane_scratch_per_value(b.max_len);
     const auto bits_at = [&](uint64_t ch) { return ((ch * cstride * 2u) + 255u) & ~255ull; };
-    /* + 256 bytes for the persistent parse's work counter */
-    const auto work_at = [&](uint64_t ch) { return (bits_at(ch) + ch * bstride * 4u + 255u) & ~255ull; };
-    while (chunk && work_at(chunk) + 256u > half) chunk--;
+    while (chunk && bits_at(chunk) + chunk * bstride * 4u > half) chunk--;
     if (chunk == 0) return hipErrorInvalidValue;
     if (pipe) {                       /* at least 4 chunks so the stages overlap */
         const uint64_t quarter = (b.count + 3u) / 4u;
@@ -1775,20 +1686,6 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
         sc[h].cstride = cstride;
         sc[h].bstride = bstride;
         sc[h].force_fix = force_fix;
-        sc[h].work = (uint32_t *)(base + work_at(chunk));
-    }
-    /* the persistent parse: as many 256-lane blocks as stay resident */
-    uint32_t parse_blocks = 0xFFFFFFFFu;
-    if (K2_PERSIST) {
-        int dev = 0, cus = 0, per = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)lzf_parse_lane_kernel, (int)K2_THREADS,
-                                                         0) == hipSuccess &&
-            cus > 0 && per > 0)
-            parse_blocks = (uint32_t)cus * (uint32_t)per;
-        else
-            parse_blocks = 256u * 4u;
     }
     /* the small-class kernel (diagnostic) is persistent: as many one-wave
      * workgroups as stay resident (LDS-bound), each walking the batch */
@@ -1878,14 +1775,8 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
             hipLaunchKernelGGL(lzf_parse_wave_kernel, dim3(cnt), dim3(64), 0, s2, c, sc[h]);
         else
 #endif
-        {
-            uint32_t g = (cnt + K2_THREADS - 1u) / K2_THREADS;
-            if (K2_PERSIST) {
-                if (g > parse_blocks) g = parse_blocks;
-                if ((e = hipMemsetAsync(sc[h].work, 0, sizeof(uint32_t), s2)) != hipSuccess) return e;
-            }
-            hipLaunchKernelGGL(lzf_parse_lane_kernel, dim3(g), dim3(K2_THREADS), parse_lds, s2, c, sc[h]);
-        }
+            hipLaunchKernelGGL(lzf_parse_lane_kernel, dim3((cnt + K2_THREADS - 1u) / K2_THREADS),
+                               dim3(K2_THREADS), parse_lds, s2, c, sc[h]);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (pipe && (e = hipEventRecord(ev[2 + h], aux)) != hipSuccess) return e;
     }

@@ -50,6 +50,11 @@ for st in "$@"; do
             AB_SEED=$([ $k = 0 ] && echo 0x5EED0004 || ([ $k = 2 ] && echo 0x5EED0003 || ([ $k = 3 ] && echo 0x5EED0005 || echo 0x5EED0002))) \
               timeout -k 10 600 python -u tools/ab_compress.py $k $nn $c 3 $libs > $O/abk_${k}_${nn}_${rest//:/_}.txt 2>&1 || exit 1
             grep -v amdgpu.ids $O/abk_${k}_${nn}_${rest//:/_}.txt ;;
+    prof:*) # prof:<label>:<bench args, comma-separated> -- rocprofv3 kernel trace + stats of bench.py
+            IFS=: read -r _ lab args <<< "$st"; args=${args//,/ }
+            timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_$lab -o run -- python3 bench.py $args --no-cpu > $O/prof_$lab.log 2>&1 || exit 1
+            python3 profiles/summarize.py $O/prof_$lab "bench.py $args (round 4)" > $O/kernel_stats_$lab.txt || exit 1
+            rm -rf $O/prof_$lab; head -6 $O/kernel_stats_$lab.txt; grep '^{' $O/prof_$lab.log | tail -1 | cut -c1-300 ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
