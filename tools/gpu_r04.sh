@@ -55,6 +55,11 @@ for st in "$@"; do
             timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_$lab -o run -- python3 bench.py $args --no-cpu > $O/prof_$lab.log 2>&1 || exit 1
             python3 profiles/summarize.py $O/prof_$lab "bench.py $args (round 4)" > $O/kernel_stats_$lab.txt || exit 1
             rm -rf $O/prof_$lab; head -6 $O/kernel_stats_$lab.txt; grep '^{' $O/prof_$lab.log | tail -1 | cut -c1-300 ;;
+    pmc:*)  # pmc:<label>:<bench args, comma-separated> -- FETCH_SIZE and WRITE_SIZE passes (one counter set per run)
+            IFS=: read -r _ lab args <<< "$st"; args=${args//,/ }
+            for c in FETCH_SIZE WRITE_SIZE; do
+              timeout -s KILL 600 rocprofv3 --pmc $c --output-format csv -d $O/pmc_${lab}_$c -o run -- python3 bench.py $args --no-cpu > $O/pmc_${lab}_$c.log 2>&1 || exit 1
+              tail -1 $O/pmc_${lab}_$c.log | cut -c1-200; done ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
