@@ -328,11 +328,17 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, uint32_t l)
     return ((uint64_t)readlane_u32((uint32_t)(v >> 32), l) << 32) | readlane_u32((uint32_t)v, l);
 }
 
-template <typename HeadT, bool WRAP>
+/* one instance per ring size, with static LDS: the compiler folds the LDS
+ * base into every address (with dynamic LDS it adds the base, 0, with one
+ * VALU per LDS address) */
+#define CW_LDS(HeadT, RING) ((RING) + CW_HBUCKETS * sizeof(HeadT) + CW_TBYTES + \
+                             ((RING) < CW_CHAIN ? (RING) : CW_CHAIN) * sizeof(uint16_t))
+template <typename HeadT, bool WRAP, uint32_t RING>
 __global__ __launch_bounds__(64) void lzf_compress_window_kernel(LzfBatch bt, uint32_t ring_bytes)
 {
     typedef HeadOps<HeadT> H;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[CW_LDS(HeadT, RING)];
+    ring_bytes = RING;
     CwLds<HeadT, WRAP> L;
     L.ring = smem;
     L.rmask = ring_bytes - 1u;
@@ -796,26 +802,28 @@ static uint32_t ring_for(uint32_t max_len)
     return r;
 }
 
-template <typename HeadT, bool WRAP>
+template <typename HeadT, bool WRAP, uint32_t RING>
 static hipError_t launch_window(const LzfBatch &b, hipStream_t s)
 {
-    const uint32_t ring = ring_for(b.max_len);
-    const uint32_t chain = ring < CW_CHAIN ? ring : CW_CHAIN;
-    const size_t lds = ring + CW_HBUCKETS * sizeof(HeadT) + CW_TBYTES +
-                       chain * sizeof(uint16_t);
-    hipError_t e = hipFuncSetAttribute((const void *)lzf_compress_window_kernel<HeadT, WRAP>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    lzf_compress_window_kernel<HeadT, WRAP><<<dim3(b.count), dim3(CW_LANES), lds, s>>>(b, ring);
+    lzf_compress_window_kernel<HeadT, WRAP, RING><<<dim3(b.count), dim3(CW_LANES), 0, s>>>(b, RING);
     return hipGetLastError();
 }
 
 hipError_t lzf_launch_compress(const LzfBatch &b, hipStream_t s)
 {
     /* values that fit the chain (8 KiB) never wrap the ring or the chain */
-    if (b.max_len <= CW_CHAIN) return launch_window<uint32_t, false>(b, s);
-    if (b.max_len <= 65536u) return launch_window<uint32_t, true>(b, s);
-    return launch_window<unsigned long long, true>(b, s);
+    static_assert(CW_CHAIN == 8192u && CW_RING_MAX == 16384u, "the instances below");
+    switch (b.max_len <= CW_CHAIN ? ring_for(b.max_len) : 0u) {
+    case 256u: return launch_window<uint32_t, false, 256u>(b, s);
+    case 512u: return launch_window<uint32_t, false, 512u>(b, s);
+    case 1024u: return launch_window<uint32_t, false, 1024u>(b, s);
+    case 2048u: return launch_window<uint32_t, false, 2048u>(b, s);
+    case 4096u: return launch_window<uint32_t, false, 4096u>(b, s);
+    case 8192u: return launch_window<uint32_t, false, 8192u>(b, s);
+    default: break;
+    }
+    if (b.max_len <= 65536u) return launch_window<uint32_t, true, CW_RING_MAX>(b, s);
+    return launch_window<unsigned long long, true, CW_RING_MAX>(b, s);
 }
 
 const char *lzf_compress_kernel_name(void) { return "window64"; }

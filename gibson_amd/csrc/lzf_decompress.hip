@@ -201,6 +201,51 @@ __device__ __forceinline__ uint32_t cd_discover(const uint8_t *inr, uint32_t ima
     return x;
 }
 
+/* step 1 with the jump table in LDS (the pipe; CD_JLDS): jt holds 256 bytes,
+ * J(p) for the round's positions p < 128 and 255 ("leaves the round") at
+ * [128, 256), so a jump is one ds_read_u8 at the entry itself.  Level b's
+ * table is read at J_b(p) to make J_{b+1} and at the lane's rank walk x, and
+ * overwritten in place: one wave's LDS operations execute in order, so every
+ * lane's reads of level b precede the write.  The rank walk applies level b
+ * as the table reaches it (the levels are powers of one map, so they commute):
+ * four LDS operations per level against two ds_bpermute and their byte
+ * extraction per table level plus one per rank level. */
+#ifndef CD_JLDS
+#define CD_JLDS 1
+#endif
+__device__ __forceinline__ uint32_t cd_discover_lds(const uint8_t *inr, uint32_t imask, uint8_t *jt, uint32_t base,
+                                                    uint32_t in_len, uint32_t lane, uint32_t &nbase)
+{
+    const uint32_t pa = 2u * lane, pb = pa + 1u;
+    const uint32_t ca = inr[(base + pa) & imask], cb = inr[(base + pb) & imask];
+    const uint32_t ta = cd_tsz(ca), tb = cd_tsz(cb);
+    uint32_t na = pa + ta, nb = pb + tb;
+    const uint32_t ipa = base + pa;
+    if (ipa + ta >= in_len || na >= CD_ROUND) na = 255u;
+    if (ipa + 1u + tb >= in_len || nb >= CD_ROUND) nb = 255u;
+    *(uint16_t *)(jt + pa) = (uint16_t)(na | (nb << 8));
+    cd_fence();
+    uint32_t x = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 6u; b++) {
+        const uint32_t jx = jt[x];
+        if (b < 5u) {
+            na = jt[na];
+            nb = jt[nb];
+            cd_fence();
+            *(uint16_t *)(jt + pa) = (uint16_t)(na | (nb << 8));
+            cd_fence();
+        }
+        x = ((lane >> b) & 1u) ? jx : x;
+    }
+    if (x >= CD_ROUND) x = CD_ROUND;
+    const bool tok = x < CD_ROUND;
+    const uint32_t ntok = (uint32_t)__builtin_popcountll(__ballot(tok));
+    const uint32_t c = inr[(base + (tok ? x : 0u)) & imask];
+    nbase = base + cd_rl(x + cd_tsz(c), ntok - 1u);
+    return x;
+}
+
 /* steps 2-3 for lane l's token: its output offset within the round (rel),
  * the owner info of its output bytes (tinfo: literal -> input ring index
  * o + tinfo, flagged in bit 31; back-ref -> distance), the round's output
@@ -301,6 +346,9 @@ __device__ __forceinline__ void cd_flush(const uint8_t *lds, uint32_t outr_off, 
 #ifndef CD_PERIOD
 #define CD_PERIOD 1
 #endif
+#ifndef CD_MARKNB
+#define CD_MARKNB 1
+#endif
 template <uint32_t IN_RING, bool PER = false>
 __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint32_t omask, uint32_t *mark,
                                              uint32_t sink_off, uint8_t *dst, uint32_t O, uint32_t total, bool tok,
@@ -317,12 +365,16 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
 #endif
     for (uint32_t g = 0; g < total; g += CD_LANES) {
         const uint32_t gb = O + g;                     /* group's first output offset */
-        if (tok && Ot - gb < CD_LANES) mark[Ot - gb] = gb + 1u;
+        if (CD_MARKNB)       /* without a branch: other lanes mark slot 64 (never read) */
+            mark[tok && Ot - gb < CD_LANES ? Ot - gb : CD_LANES] = gb + 1u;
+        else if (tok && Ot - gb < CD_LANES)
+            mark[Ot - gb] = gb + 1u;
         cd_fence();
-        const uint64_t S = __ballot(mark[lane] == gb + 1u);
+        const bool mine = mark[lane] == gb + 1u;
+        const uint64_t S = __ballot(mine);
         const uint32_t le = __builtin_amdgcn_mbcnt_hi((uint32_t)(S >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)S, 0u)) +
-                            (uint32_t)((S >> lane) & 1ull);
+                            (mine ? 1u : 0u);
         const uint32_t k = tbase + le - 1u;
         tbase += (uint32_t)__builtin_popcountll(S);
         const uint32_t tInf = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)tinfo);
@@ -344,9 +396,16 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
         const uint32_t a = (((o + tInf) & imask) & lit) | ((outr_off + (so & omask)) & ~lit);
         const uint32_t q = so - gb;
         const uint32_t b = lds[a];
-        uint32_t ent = (!lit && q < CD_LANES) ? (q << 8) : (0x10000u | b);
-        while (__ballot(!(ent & 0x10000u)))
-            ent = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((ent & 0x10000u) ? lane : (ent >> 8)) << 2), (int)ent);
+        /* resolved: bit 31 | the byte; pending: the source lane's ds_bpermute
+         * address (lane × 4) in bits 10-15 */
+        const bool pend = !lit && q < CD_LANES;
+        int32_t ent = pend ? (int32_t)(q << 10) : (int32_t)(0x80000000u | b);
+        if (__ballot(pend)) {
+            const int32_t me = (int32_t)(lane << 2);
+            do
+                ent = __builtin_amdgcn_ds_bpermute(ent < 0 ? me : ent >> 8, ent);
+            while (__ballot(ent >= 0));
+        }
         const bool live = g + lane < total;
         lds[live ? outr_off + (o & omask) : sink_off] = (uint8_t)ent;
         cd_fence();
@@ -498,13 +557,17 @@ __device__ __forceinline__ bool cd_refused(const LzfBatch &bt, uint32_t v, uint3
     return true;
 }
 
+/* one instance per window size, with static LDS (as the pipe) */
+template <uint32_t RING>
 __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, uint32_t out_ring)
 {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[CD_IN_RING1 + RING + CD_LANES * 5u + (CD_JLDS ? 256u : 0u)];
+    out_ring = RING;
     uint8_t *inr = smem;                               /* CD_IN_RING1 */
     uint8_t *outr = smem + CD_IN_RING1;                /* out_ring (power of two) */
     uint32_t *mark = (uint32_t *)(outr + out_ring);    /* 64 token-start marks (group tags) */
-    uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* the walk's token starts, in order */
+    uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* the idle lanes' byte sink */
+    uint8_t *jt = tokpos + CD_LANES;                   /* CD_JLDS: the jump table */
     const uint32_t imask = CD_IN_RING1 - 1u, omask = out_ring - 1u;
 
     const uint32_t lane = threadIdx.x;
@@ -518,6 +581,7 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
     const uint32_t avail = in_len ? in_len : 1u;
 
     mark[lane] = 0u;            /* group tags are >= 1 */
+    if (CD_JLDS) *(uint16_t *)(jt + CD_ROUND + 2u * lane) = 0xFFFFu;
     uint32_t loaded = 0, base = 0, O = 0;
     uint32_t F = 0;             /* output [0, F) stored */
     int32_t err = 0;
@@ -526,7 +590,8 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
         first = false;
         cd_stage<CD_IN_RING1>(inr, src, base, avail, loaded, lane);
         uint32_t nbase;
-        const uint32_t x = cd_discover(inr, imask, tokpos, base, in_len, lane, nbase);
+        const uint32_t x = CD_JLDS ? cd_discover_lds(inr, imask, jt, base, in_len, lane, nbase)
+                                   : cd_discover(inr, imask, tokpos, base, in_len, lane, nbase);
         const CdRound r = cd_decode(inr, imask, base, x, O, in_len, cap);
         if (r.err) {
             err = r.err;
@@ -571,15 +636,29 @@ __device__ __forceinline__ void cd_stage_pipe(uint8_t *inr, const uint8_t *src, 
     }
 }
 
+/* the pipe's window is always CD_OUT_MAX (values over 4 KiB), so its LDS is
+ * static: the compiler folds the LDS base into every address (with dynamic
+ * LDS it adds the base, 0, with one VALU per LDS address) */
+#ifndef CD_PIPE_STATIC
+#define CD_PIPE_STATIC 1
+#endif
+#define CD_PIPE_LDS (CD_IN_RINGP + 2u * sizeof(CdSlot) + 5u * CD_LANES + 16u + CD_OUT_MAX + \
+                     (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u) + (CD_JLDS ? 256u : 0u))
 __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, uint32_t out_ring)
 {
+#if CD_PIPE_STATIC
+    __shared__ __attribute__((aligned(16))) uint8_t smem[CD_PIPE_LDS];
+    out_ring = CD_OUT_MAX;
+#else
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+#endif
     uint8_t *inr = smem;                               /* CD_IN_RINGP (+ the mirror, CD_TOKOUT) */
     CdSlot *slot = (CdSlot *)(smem + CD_IN_RINGP + (CD_TOKOUT ? CD_IN_MIRROR : 0u));   /* 2 */
     uint32_t *mark = (uint32_t *)(slot + 2);           /* the consumer's 64 token-start marks */
     uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* unused (was the removed walk's token starts) */
     uint8_t *sink = tokpos + CD_LANES;                 /* the consumer's idle-lane byte sink */
     uint8_t *outr = sink + 16u;                        /* out_ring (power of two) */
+    uint8_t *jt = outr + out_ring;                     /* CD_JLDS: the producer's jump table */
     const uint32_t imask = CD_IN_RINGP - 1u, omask = out_ring - 1u;
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -599,10 +678,12 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
         const uint8_t *src = bt.in + bt.in_off[v];
         const uint32_t avail = in_len ? in_len : 1u;   /* a 0-length stream still reads one byte */
         uint32_t loaded = 0, base = 0, O = 0;
+        if (CD_JLDS) *(uint16_t *)(jt + CD_ROUND + 2u * lane) = 0xFFFFu;
         for (uint32_t k = 0;; k++) {
             cd_stage_pipe(inr, src, base, avail, loaded, lane);
             uint32_t nbase;
-            const uint32_t x = cd_discover(inr, imask, tokpos, base, in_len, lane, nbase);
+            const uint32_t x = CD_JLDS ? cd_discover_lds(inr, imask, jt, base, in_len, lane, nbase)
+                                       : cd_discover(inr, imask, tokpos, base, in_len, lane, nbase);
             const CdRound r = cd_decode(inr, imask, base, x, O, in_len, cap);
             const uint32_t ntok = (uint32_t)__builtin_popcountll(__ballot(x < CD_ROUND));
             const uint32_t total = r.total;
@@ -683,18 +764,28 @@ hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s)
     if (CD_PIPE && ring >= CD_PIPE_MIN_RING) {
         /* CD_TOKOUT: + the input ring's mirror and 16 bytes past the window
          * (a 16-byte read near its end) */
-        const size_t lds = CD_IN_RINGP + 2u * sizeof(CdSlot) + 5u * CD_LANES + 16u + ring +
-                           (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u);
-        e = hipFuncSetAttribute((const void *)lzf_decompress_pipe_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
+        size_t lds = CD_IN_RINGP + 2u * sizeof(CdSlot) + 5u * CD_LANES + 16u + ring +
+                     (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u) + (CD_JLDS ? 256u : 0u);
+        if (CD_PIPE_STATIC) {
+            if (ring != CD_OUT_MAX) return hipErrorInvalidValue;
+            lds = 0;
+        } else {
+            e = hipFuncSetAttribute((const void *)lzf_decompress_pipe_kernel,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
         hipLaunchKernelGGL(lzf_decompress_pipe_kernel, dim3(b.count), dim3(2u * CD_LANES), lds, s, b, ring);
     } else {
-        const size_t lds = CD_IN_RING1 + ring + CD_LANES * 5u;     /* + the 64 marks and token starts */
-        e = hipFuncSetAttribute((const void *)lzf_decompress_tokpar_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(lzf_decompress_tokpar_kernel, dim3(b.count), dim3(CD_LANES), lds, s, b, ring);
+        /* LDS: the input ring, the window, the 64 marks and token starts */
+        switch (ring) {
+        case 256u: hipLaunchKernelGGL(lzf_decompress_tokpar_kernel<256u>, dim3(b.count), dim3(CD_LANES), 0, s, b, ring); break;
+        case 512u: hipLaunchKernelGGL(lzf_decompress_tokpar_kernel<512u>, dim3(b.count), dim3(CD_LANES), 0, s, b, ring); break;
+        case 1024u: hipLaunchKernelGGL(lzf_decompress_tokpar_kernel<1024u>, dim3(b.count), dim3(CD_LANES), 0, s, b, ring); break;
+        case 2048u: hipLaunchKernelGGL(lzf_decompress_tokpar_kernel<2048u>, dim3(b.count), dim3(CD_LANES), 0, s, b, ring); break;
+        case 4096u: hipLaunchKernelGGL(lzf_decompress_tokpar_kernel<4096u>, dim3(b.count), dim3(CD_LANES), 0, s, b, ring); break;
+        case 8192u: hipLaunchKernelGGL(lzf_decompress_tokpar_kernel<8192u>, dim3(b.count), dim3(CD_LANES), 0, s, b, ring); break;
+        default: return hipErrorInvalidValue;
+        }
     }
     return hipGetLastError();
 }
