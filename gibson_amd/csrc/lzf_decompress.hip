@@ -80,6 +80,10 @@ __device__ __forceinline__ uint4 cd_ld16(const uint8_t *p, uint32_t avail)
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+/* the wave's lane mask of a predicate, straight from the compare (HIP's
+ * __ballot takes an int, which can cost a select and a compare per use) */
+__device__ __forceinline__ uint64_t cd_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
 __device__ __forceinline__ void cd_fence()
 {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -195,7 +199,7 @@ __device__ __forceinline__ uint32_t cd_discover(const uint8_t *inr, uint32_t ima
     if (x >= CD_ROUND) x = CD_ROUND;
     /* the next round starts after the last token */
     const bool tok = x < CD_ROUND;
-    const uint32_t ntok = (uint32_t)__builtin_popcountll(__ballot(tok));
+    const uint32_t ntok = (uint32_t)__builtin_popcountll(cd_ballot(tok));
     const uint32_t c = inr[(base + (tok ? x : 0u)) & imask];
     nbase = base + cd_rl(x + cd_tsz(c), ntok - 1u);
     return x;
@@ -214,7 +218,7 @@ __device__ __forceinline__ uint32_t cd_discover(const uint8_t *inr, uint32_t ima
 #define CD_JLDS 1
 #endif
 __device__ __forceinline__ uint32_t cd_discover_lds(const uint8_t *inr, uint32_t imask, uint8_t *jt, uint32_t base,
-                                                    uint32_t in_len, uint32_t lane, uint32_t &nbase)
+                                                    uint32_t in_len, uint32_t lane)
 {
     const uint32_t pa = 2u * lane, pb = pa + 1u;
     const uint32_t ca = inr[(base + pa) & imask], cb = inr[(base + pb) & imask];
@@ -238,12 +242,7 @@ __device__ __forceinline__ uint32_t cd_discover_lds(const uint8_t *inr, uint32_t
         }
         x = ((lane >> b) & 1u) ? jx : x;
     }
-    if (x >= CD_ROUND) x = CD_ROUND;
-    const bool tok = x < CD_ROUND;
-    const uint32_t ntok = (uint32_t)__builtin_popcountll(__ballot(tok));
-    const uint32_t c = inr[(base + (tok ? x : 0u)) & imask];
-    nbase = base + cd_rl(x + cd_tsz(c), ntok - 1u);
-    return x;
+    return x >= CD_ROUND ? CD_ROUND : x;
 }
 
 /* steps 2-3 for lane l's token: its output offset within the round (rel),
@@ -255,6 +254,7 @@ __device__ __forceinline__ uint32_t cd_discover_lds(const uint8_t *inr, uint32_t
 #endif
 struct CdRound {
     uint32_t rel, tinfo, total;
+    uint32_t nbase;          /* the input offset after the round's last token */
     int32_t err;
     bool overlap;            /* a back-reference of the round repeats its distance CD_PER_RATIO times */
 };
@@ -278,6 +278,9 @@ __device__ __forceinline__ CdRound cd_decode(const uint8_t *inr, uint32_t imask,
     const uint32_t Ot = O + r.rel;                      /* output offset of my token */
     r.tinfo = lit ? (((lsrc - Ot) & 0x7FFFFFFFu) | 0x80000000u) : back;
     r.total = cd_rl(incl, 63u);
+    /* the round's last token (lane ntok - 1: tokens fill the low lanes) ends the round */
+    const uint32_t ntok = (uint32_t)__builtin_popcountll(cd_ballot(tok));
+    r.nbase = base + cd_rl(x + (lit ? c + 2u : (l7 ? 3u : 2u)), ntok - 1u);
     /* away from the stream's end (every token byte of the round, at most
      * base + CD_ROUND + 32, lies inside the input) and with the round's output
      * inside the cap, only a back-reference before the output start can fail */
@@ -295,11 +298,11 @@ __device__ __forceinline__ CdRound cd_decode(const uint8_t *inr, uint32_t imask,
             else if (back > Ot) e = 22;                                     /* :127 */
         }
     }
-    const uint64_t EB = __ballot(e != 0);
+    const uint64_t EB = cd_ballot(e != 0);
     r.err = EB ? (int32_t)cd_rl((uint32_t)e, (uint32_t)__builtin_ctzll(EB)) : 0;
     /* a run long enough that the shortcut saves doubling steps (CD_PER_RATIO
      * periods or more) */
-    r.overlap = __ballot(tok && !lit && olen >= CD_PER_RATIO * back) != 0ull;
+    r.overlap = cd_ballot(tok && !lit && olen >= CD_PER_RATIO * back) != 0ull;
     return r;
 }
 
@@ -371,7 +374,7 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
             mark[Ot - gb] = gb + 1u;
         cd_fence();
         const bool mine = mark[lane] == gb + 1u;
-        const uint64_t S = __ballot(mine);
+        const uint64_t S = cd_ballot(mine);
         const uint32_t le = __builtin_amdgcn_mbcnt_hi((uint32_t)(S >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)S, 0u)) +
                             (mine ? 1u : 0u);
@@ -393,18 +396,21 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
                 so = ot - tInf + (uint32_t)r;
             }
         }
-        const uint32_t a = (((o + tInf) & imask) & lit) | ((outr_off + (so & omask)) & ~lit);
+        /* the input ring lies right after the window */
+        const uint32_t li = IN_RING <= omask + 1u ? ((o + tInf) & imask) | (omask + 1u)
+                                                  : ((o + tInf) & imask) + (omask + 1u);
+        const uint32_t a = outr_off + ((li & lit) | ((so & omask) & ~lit));
         const uint32_t q = so - gb;
         const uint32_t b = lds[a];
         /* resolved: bit 31 | the byte; pending: the source lane's ds_bpermute
          * address (lane × 4) in bits 10-15 */
         const bool pend = !lit && q < CD_LANES;
         int32_t ent = pend ? (int32_t)(q << 10) : (int32_t)(0x80000000u | b);
-        if (__ballot(pend)) {
+        if (cd_ballot(pend)) {
             const int32_t me = (int32_t)(lane << 2);
             do
                 ent = __builtin_amdgcn_ds_bpermute(ent < 0 ? me : ent >> 8, ent);
-            while (__ballot(ent >= 0));
+            while (cd_ballot(ent >= 0));
         }
         const bool live = g + lane < total;
         lds[live ? outr_off + (o & omask) : sink_off] = (uint8_t)ent;
@@ -505,7 +511,7 @@ __device__ __forceinline__ void cd_output_tok(uint8_t *inr, uint8_t *outr, uint8
     const uint32_t e = lit ? 0u : (s + len < Ot ? s + len : Ot);
     bool done = !act;
     for (;;) {
-        const uint64_t D = __ballot(done);
+        const uint64_t D = cd_ballot(done);
         if (D == ~0ull) break;
         const uint64_t before = ~D & ((1ull << lane) - 1ull);
         const uint32_t js = before ? 63u - (uint32_t)__builtin_clzll(before) : 0u;
@@ -563,9 +569,9 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
 {
     __shared__ __attribute__((aligned(16))) uint8_t smem[CD_IN_RING1 + RING + CD_LANES * 5u + (CD_JLDS ? 256u : 0u)];
     out_ring = RING;
-    uint8_t *inr = smem;                               /* CD_IN_RING1 */
-    uint8_t *outr = smem + CD_IN_RING1;                /* out_ring (power of two) */
-    uint32_t *mark = (uint32_t *)(outr + out_ring);    /* 64 token-start marks (group tags) */
+    uint8_t *outr = smem;                              /* out_ring (power of two) */
+    uint8_t *inr = outr + out_ring;                    /* CD_IN_RING1, right after the window (cd_output) */
+    uint32_t *mark = (uint32_t *)(inr + CD_IN_RING1);  /* 64 token-start marks (group tags) */
     uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* the idle lanes' byte sink */
     uint8_t *jt = tokpos + CD_LANES;                   /* CD_JLDS: the jump table */
     const uint32_t imask = CD_IN_RING1 - 1u, omask = out_ring - 1u;
@@ -589,20 +595,20 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
     while (first || base < in_len) {                     /* src/lzf_d.c:64, 146 */
         first = false;
         cd_stage<CD_IN_RING1>(inr, src, base, avail, loaded, lane);
-        uint32_t nbase;
-        const uint32_t x = CD_JLDS ? cd_discover_lds(inr, imask, jt, base, in_len, lane, nbase)
-                                   : cd_discover(inr, imask, tokpos, base, in_len, lane, nbase);
+        uint32_t nb0;
+        const uint32_t x = CD_JLDS ? cd_discover_lds(inr, imask, jt, base, in_len, lane)
+                                   : cd_discover(inr, imask, tokpos, base, in_len, lane, nb0);
         const CdRound r = cd_decode(inr, imask, base, x, O, in_len, cap);
         if (r.err) {
             err = r.err;
             break;
         }
-        cd_output<CD_IN_RING1>(smem, CD_IN_RING1, omask, mark, (uint32_t)(tokpos - smem), dst, O, r.total,
+        cd_output<CD_IN_RING1>(smem, 0u, omask, mark, (uint32_t)(tokpos - smem), dst, O, r.total,
                                x < CD_ROUND, O + r.rel, r.tinfo, lane, F);
         O += r.total;
-        base = nbase;
+        base = r.nbase;
     }
-    cd_flush(smem, CD_IN_RING1, omask, dst, F, O, lane);   /* the rounds before a failing one, as the reference */
+    cd_flush(smem, 0u, omask, dst, F, O, lane);   /* the rounds before a failing one, as the reference */
     if (lane == 0) {
         bt.out_len[v] = err ? 0u : O;
         bt.err[v] = err;
@@ -652,13 +658,14 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
 #else
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 #endif
-    uint8_t *inr = smem;                               /* CD_IN_RINGP (+ the mirror, CD_TOKOUT) */
-    CdSlot *slot = (CdSlot *)(smem + CD_IN_RINGP + (CD_TOKOUT ? CD_IN_MIRROR : 0u));   /* 2 */
+    CdSlot *slot = (CdSlot *)smem;                     /* 2 */
     uint32_t *mark = (uint32_t *)(slot + 2);           /* the consumer's 64 token-start marks */
     uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* unused (was the removed walk's token starts) */
     uint8_t *sink = tokpos + CD_LANES;                 /* the consumer's idle-lane byte sink */
     uint8_t *outr = sink + 16u;                        /* out_ring (power of two) */
-    uint8_t *jt = outr + out_ring;                     /* CD_JLDS: the producer's jump table */
+    uint8_t *inr = outr + out_ring;                    /* CD_IN_RINGP, right after the window (cd_output);
+                                                          CD_TOKOUT: + the mirror and 16 bytes */
+    uint8_t *jt = inr + CD_IN_RINGP + (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u);   /* CD_JLDS: the jump table */
     const uint32_t imask = CD_IN_RINGP - 1u, omask = out_ring - 1u;
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -681,15 +688,15 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
         if (CD_JLDS) *(uint16_t *)(jt + CD_ROUND + 2u * lane) = 0xFFFFu;
         for (uint32_t k = 0;; k++) {
             cd_stage_pipe(inr, src, base, avail, loaded, lane);
-            uint32_t nbase;
-            const uint32_t x = CD_JLDS ? cd_discover_lds(inr, imask, jt, base, in_len, lane, nbase)
-                                       : cd_discover(inr, imask, tokpos, base, in_len, lane, nbase);
+            uint32_t nb0;
+            const uint32_t x = CD_JLDS ? cd_discover_lds(inr, imask, jt, base, in_len, lane)
+                                       : cd_discover(inr, imask, tokpos, base, in_len, lane, nb0);
             const CdRound r = cd_decode(inr, imask, base, x, O, in_len, cap);
-            const uint32_t ntok = (uint32_t)__builtin_popcountll(__ballot(x < CD_ROUND));
+            const uint32_t ntok = (uint32_t)__builtin_popcountll(cd_ballot(x < CD_ROUND));
             const uint32_t total = r.total;
             CdSlot &s = slot[k & 1u];
             s.tok[lane] = (r.rel & 0xFFFFu) | ((r.tinfo >> 31) << 16) | ((r.tinfo & 0x7FFFu) << 17);
-            const bool last = r.err != 0 || nbase >= in_len;   /* src/lzf_d.c:146 */
+            const bool last = r.err != 0 || r.nbase >= in_len;   /* src/lzf_d.c:146 */
             if (lane == 0) {
                 s.ntok = ntok;
                 s.total = total;
@@ -697,7 +704,7 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
                 s.err = r.err;
             }
             O += total;
-            base = nbase;
+            base = r.nbase;
             cd_barrier(tw);
             if (last) break;
         }

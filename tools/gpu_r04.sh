@@ -60,6 +60,10 @@ for st in "$@"; do
             for c in FETCH_SIZE WRITE_SIZE; do
               timeout -s KILL 600 rocprofv3 --pmc $c --output-format csv -d $O/pmc_${lab}_$c -o run -- python3 bench.py $args --no-cpu > $O/pmc_${lab}_$c.log 2>&1 || exit 1
               tail -1 $O/pmc_${lab}_$c.log | cut -c1-200; done ;;
+    tstat:*) # tstat:<kind>:<n>:<count> -- pipe phase cycles (CD_TIMING build liblzf_hip_time.so)
+            IFS=: read -r _ k nn c <<< "$st"
+            timeout -k 10 300 python -u tools/dec_tstat.py $k $nn $c gibson_amd/liblzf_hip_time.so > $O/tstat_${k}_${nn}.txt 2>&1 || exit 1
+            grep -v amdgpu.ids $O/tstat_${k}_${nn}.txt ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
