@@ -217,16 +217,36 @@ __device__ __forceinline__ uint32_t cd_discover(const uint8_t *inr, uint32_t ima
 #ifndef CD_JLDS
 #define CD_JLDS 1
 #endif
+#ifndef CD_TSZT
+#define CD_TSZT 1
+#endif
+#ifndef CD_PREF
+#define CD_PREF 1
+#endif
+/* CD_TSZT: token sizes from a 256-byte LDS table, tszt[c] = cd_tsz(c), at jt + 256 */
+__device__ __forceinline__ void cd_tszt_init(uint8_t *jt, uint32_t lane)
+{
+    if (CD_TSZT) {
+        const uint32_t c = 4u * lane;
+        *(uint32_t *)(jt + 256u + c) = cd_tsz(c) | (cd_tsz(c + 1u) << 8) | (cd_tsz(c + 2u) << 16) | (cd_tsz(c + 3u) << 24);
+    }
+}
 __device__ __forceinline__ uint32_t cd_discover_lds(const uint8_t *inr, uint32_t imask, uint8_t *jt, uint32_t base,
                                                     uint32_t in_len, uint32_t lane)
 {
     const uint32_t pa = 2u * lane, pb = pa + 1u;
     const uint32_t ca = inr[(base + pa) & imask], cb = inr[(base + pb) & imask];
-    const uint32_t ta = cd_tsz(ca), tb = cd_tsz(cb);
+    const uint32_t ta = CD_TSZT ? jt[256u + ca] : cd_tsz(ca), tb = CD_TSZT ? jt[256u + cb] : cd_tsz(cb);
+    /* J0 = the next token's start: any entry >= 128 leaves the round (the
+     * table holds 255 there, so its first jump gives 255); away from the
+     * stream's end no token crosses in_len, so only near it are entries
+     * clamped (a round's last token ends at most 127 + 33 bytes in) */
     uint32_t na = pa + ta, nb = pb + tb;
-    const uint32_t ipa = base + pa;
-    if (ipa + ta >= in_len || na >= CD_ROUND) na = 255u;
-    if (ipa + 1u + tb >= in_len || nb >= CD_ROUND) nb = 255u;
+    if (base + CD_ROUND + 33u > in_len) {
+        const uint32_t ipa = base + pa;
+        if (ipa + ta >= in_len) na = 255u;
+        if (ipa + 1u + tb >= in_len) nb = 255u;
+    }
     *(uint16_t *)(jt + pa) = (uint16_t)(na | (nb << 8));
     cd_fence();
     uint32_t x = 0;
@@ -567,7 +587,8 @@ __device__ __forceinline__ bool cd_refused(const LzfBatch &bt, uint32_t v, uint3
 template <uint32_t RING>
 __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, uint32_t out_ring)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[CD_IN_RING1 + RING + CD_LANES * 5u + (CD_JLDS ? 256u : 0u)];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[CD_IN_RING1 + RING + CD_LANES * 5u +
+                                                         (CD_JLDS ? (CD_TSZT ? 512u : 256u) : 0u)];
     out_ring = RING;
     uint8_t *outr = smem;                              /* out_ring (power of two) */
     uint8_t *inr = outr + out_ring;                    /* CD_IN_RING1, right after the window (cd_output) */
@@ -587,7 +608,10 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
     const uint32_t avail = in_len ? in_len : 1u;
 
     mark[lane] = 0u;            /* group tags are >= 1 */
-    if (CD_JLDS) *(uint16_t *)(jt + CD_ROUND + 2u * lane) = 0xFFFFu;
+    if (CD_JLDS) {
+        *(uint16_t *)(jt + CD_ROUND + 2u * lane) = 0xFFFFu;
+        cd_tszt_init(jt, lane);
+    }
     uint32_t loaded = 0, base = 0, O = 0;
     uint32_t F = 0;             /* output [0, F) stored */
     int32_t err = 0;
@@ -649,7 +673,7 @@ __device__ __forceinline__ void cd_stage_pipe(uint8_t *inr, const uint8_t *src, 
 #define CD_PIPE_STATIC 1
 #endif
 #define CD_PIPE_LDS (CD_IN_RINGP + 2u * sizeof(CdSlot) + 5u * CD_LANES + 16u + CD_OUT_MAX + \
-                     (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u) + (CD_JLDS ? 256u : 0u))
+                     (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u) + (CD_JLDS ? (CD_TSZT ? 512u : 256u) : 0u))
 __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, uint32_t out_ring)
 {
 #if CD_PIPE_STATIC
@@ -672,8 +696,8 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
     const bool producer = threadIdx.x < 64u;
     const uint32_t v = blockIdx.x;
     if ((bt.skip && bt.skip[v]) || cd_refused(bt, v, threadIdx.x)) return;
-    const uint32_t in_len = bt.in_len[v];
-    const uint32_t cap = bt.out_cap[v];
+    const uint32_t in_len = __builtin_amdgcn_readfirstlane(bt.in_len[v]);   /* scalar: no load wait in the loop */
+    const uint32_t cap = __builtin_amdgcn_readfirstlane(bt.out_cap[v]);
 
     uint64_t tw[3] = {0ull, 0ull, 0ull};
 #ifdef CD_TIMING
@@ -685,9 +709,41 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
         const uint8_t *src = bt.in + bt.in_off[v];
         const uint32_t avail = in_len ? in_len : 1u;   /* a 0-length stream still reads one byte */
         uint32_t loaded = 0, base = 0, O = 0;
-        if (CD_JLDS) *(uint16_t *)(jt + CD_ROUND + 2u * lane) = 0xFFFFu;
+        if (CD_JLDS) {
+            *(uint16_t *)(jt + CD_ROUND + 2u * lane) = 0xFFFFu;
+            cd_tszt_init(jt, lane);
+        }
+        /* CD_PREF: the input the next round needs is loaded at the start of
+         * this round and written to the ring when the next round starts, so
+         * its load latency is off the producer's chain (the synchronous stage
+         * then runs in round 0 only) */
+        uint4 pv = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t pto = 0u;
+        bool pend = false;
         for (uint32_t k = 0;; k++) {
+            if (CD_PREF && pend) {
+                const uint32_t px = loaded + 16u * lane;
+                if (px < pto) {
+                    *(uint4 *)(inr + (px & (CD_IN_RINGP - 1u))) = pv;
+                    if (CD_TOKOUT && (px & (CD_IN_RINGP - 1u)) < CD_IN_MIRROR)
+                        *(uint4 *)(inr + CD_IN_RINGP + (px & (CD_IN_RINGP - 1u))) = pv;
+                }
+                loaded = pto;
+                pend = false;
+                cd_fence();
+            }
             cd_stage_pipe(inr, src, base, avail, loaded, lane);
+            /* the next round starts at >= base + 128 (tokens start in
+             * [base, base + 128) and the last one ends past it) and at most
+             * base + 160: the ring may take up to base + 448 at its start
+             * (the consumer then reads round k's [base, base + 161), and
+             * offset y overwrites y - 512), and needs base_{k+1} + 192 */
+            if (CD_PREF && loaded < min(avail, base + 448u) && base + 128u < in_len) {
+                pto = min(avail, (base + 448u) & ~15u);
+                const uint32_t px = loaded + 16u * lane;
+                if (px < pto) pv = cd_ld16(src + px, pto - px);
+                pend = true;
+            }
             uint32_t nb0;
             const uint32_t x = CD_JLDS ? cd_discover_lds(inr, imask, jt, base, in_len, lane)
                                        : cd_discover(inr, imask, tokpos, base, in_len, lane, nb0);
@@ -772,7 +828,7 @@ hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s)
         /* CD_TOKOUT: + the input ring's mirror and 16 bytes past the window
          * (a 16-byte read near its end) */
         size_t lds = CD_IN_RINGP + 2u * sizeof(CdSlot) + 5u * CD_LANES + 16u + ring +
-                     (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u) + (CD_JLDS ? 256u : 0u);
+                     (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u) + (CD_JLDS ? (CD_TSZT ? 512u : 256u) : 0u);
         if (CD_PIPE_STATIC) {
             if (ring != CD_OUT_MAX) return hipErrorInvalidValue;
             lds = 0;
