@@ -257,7 +257,7 @@ __device__ __forceinline__ uint32_t cd_discover_lds(const uint8_t *inr, uint32_t
             na = jt[na];
             nb = jt[nb];
             cd_fence();
-            *(uint16_t *)(jt + pa) = (uint16_t)(na | (nb << 8));
+            *(uint16_t *)(jt + pa) = (uint16_t)__builtin_amdgcn_perm(nb, na, 0x0c0c0400u);   /* na | nb << 8 */
             cd_fence();
         }
         x = ((lane >> b) & 1u) ? jx : x;
@@ -276,7 +276,8 @@ struct CdRound {
     uint32_t rel, tinfo, total;
     uint32_t nbase;          /* the input offset after the round's last token */
     int32_t err;
-    bool overlap;            /* a back-reference of the round repeats its distance CD_PER_RATIO times */
+    uint64_t overlap;        /* lanes whose back-reference repeats its distance CD_PER_RATIO times */
+    uint32_t ntok;           /* tokens of the round (lanes 0 .. ntok - 1) */
 };
 
 __device__ __forceinline__ CdRound cd_decode(const uint8_t *inr, uint32_t imask, uint32_t base, uint32_t x,
@@ -299,8 +300,8 @@ __device__ __forceinline__ CdRound cd_decode(const uint8_t *inr, uint32_t imask,
     r.tinfo = lit ? (((lsrc - Ot) & 0x7FFFFFFFu) | 0x80000000u) : back;
     r.total = cd_rl(incl, 63u);
     /* the round's last token (lane ntok - 1: tokens fill the low lanes) ends the round */
-    const uint32_t ntok = (uint32_t)__builtin_popcountll(cd_ballot(tok));
-    r.nbase = base + cd_rl(x + (lit ? c + 2u : (l7 ? 3u : 2u)), ntok - 1u);
+    r.ntok = (uint32_t)__builtin_popcountll(cd_ballot(tok));
+    r.nbase = base + cd_rl(x + (lit ? c + 2u : (l7 ? 3u : 2u)), r.ntok - 1u);
     /* away from the stream's end (every token byte of the round, at most
      * base + CD_ROUND + 32, lies inside the input) and with the round's output
      * inside the cap, only a back-reference before the output start can fail */
@@ -322,7 +323,7 @@ __device__ __forceinline__ CdRound cd_decode(const uint8_t *inr, uint32_t imask,
     r.err = EB ? (int32_t)cd_rl((uint32_t)e, (uint32_t)__builtin_ctzll(EB)) : 0;
     /* a run long enough that the shortcut saves doubling steps (CD_PER_RATIO
      * periods or more) */
-    r.overlap = cd_ballot(tok && !lit && olen >= CD_PER_RATIO * back) != 0ull;
+    r.overlap = cd_ballot(tok && !lit && olen >= CD_PER_RATIO * back);
     return r;
 }
 
@@ -748,15 +749,15 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
             const uint32_t x = CD_JLDS ? cd_discover_lds(inr, imask, jt, base, in_len, lane)
                                        : cd_discover(inr, imask, tokpos, base, in_len, lane, nb0);
             const CdRound r = cd_decode(inr, imask, base, x, O, in_len, cap);
-            const uint32_t ntok = (uint32_t)__builtin_popcountll(cd_ballot(x < CD_ROUND));
+            const uint32_t ntok = r.ntok;
             const uint32_t total = r.total;
             CdSlot &s = slot[k & 1u];
-            s.tok[lane] = (r.rel & 0xFFFFu) | ((r.tinfo >> 31) << 16) | ((r.tinfo & 0x7FFFu) << 17);
+            s.tok[lane] = (r.tinfo << 17) | ((r.tinfo >> 31) << 16) | r.rel;   /* rel < 65536 */
             const bool last = r.err != 0 || r.nbase >= in_len;   /* src/lzf_d.c:146 */
             if (lane == 0) {
                 s.ntok = ntok;
                 s.total = total;
-                s.last = (last ? 1u : 0u) | (r.overlap ? 2u : 0u);
+                s.last = (last ? 1u : 0u) | (r.overlap != 0ull ? 2u : 0u);
                 s.err = r.err;
             }
             O += total;
