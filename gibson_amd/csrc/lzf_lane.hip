@@ -932,7 +932,10 @@ extern "C" int lzf_gpu_debug_sites(unsigned long long *out16, int reset)
 #define K2_LITMIN   8u       /* lanes of the wave that must take a free-literal trip for it to run */
 #endif
 #ifndef K2_LITX
-#define K2_LITX 3u       /* free literals taken after a literal in the same iteration (0: none) */
+#define K2_LITX 2u       /* free-literal trips after a literal in the same iteration (0: none) */
+#endif
+#ifndef K2_LITB
+#define K2_LITB 1        /* a trip takes up to 4 free literals (0: one) */
 #endif
 enum { K2_STEP = 0, K2_RESOLVE = 1, K2_DECIDE = 2, K2_EXTEND = 3, K2_EMIT = 4, K2_DONE = 5 };
 
@@ -989,6 +992,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
     uint32_t rel = 0u, q = 0u, k = 0u, lim = 0u, m = 0u;
     bool ok = true;
     uint32_t mode = n >= 3u ? K2_STEP : K2_DONE;
+    [[maybe_unused]] uint32_t fm = 0u, fmb = 0xFFFFFFE0u;   /* K2_LITB: candidate mask of block fmb */
 
 /* completed dwords [fs, fw) wait in pb0..2 (slot fw - fs) and leave with
  * the fourth as one 16-byte store; slot and patch selects instead of
@@ -1159,6 +1163,59 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                      * all (one ballot of the branch's lanes): on text, where
                      * few are, the wave skips the path */
                     bool go = true;
+#if K2_LITB
+                    /* K2_LITB: up to 4 free literals per trip.  fm: bit j set
+                     * when cand word cb + j has a candidate (code != 0), made
+                     * once per block on the path's first use of it */
+                    if ((uint32_t)__builtin_popcountll(__ballot(true)) >= K2_LITMIN) {
+                        if (fmb != cb) {
+                            fm = 0u;
+#pragma unroll
+                            for (uint32_t i_ = 0; i_ < 16u; i_++) {
+                                const uint32_t w_ = ln_sel4(i_ < 4u ? C0 : i_ < 8u ? C1 : i_ < 12u ? C2 : C3, i_ & 3u);
+                                /* codes of the two words at bits 0-2 and 16-18; + 7 carries into bit 3 / 19 when nonzero */
+                                const uint32_t t_ = ((w_ >> 13) & 0x70007u) + 0x70007u;
+                                fm |= (((t_ >> 3) & 1u) | ((t_ >> 18) & 2u)) << (2u * i_);
+                            }
+                            fmb = cb;
+                        }
+#pragma unroll
+                        for (uint32_t e_ = 0; e_ < K2_LITX; e_++) {
+                            const uint32_t d_ = p - cb, x_ = p - wb;
+                            uint32_t r_ = 0u;
+                            if (go && p < n - 2u && d_ < K2_CB && x_ < 16u && o < cap) {
+                                const uint32_t z_ = fm >> d_;
+                                r_ = z_ ? (uint32_t)__builtin_ctz(z_) : 32u;
+                                r_ = min(r_, min(K2_CB - d_, 16u - x_));
+                                r_ = min(r_, min(n - 2u - p, cap - o));
+                                r_ = min(r_, min(LZF_MAX_LIT - run, 32u - (p & 31u)));
+                                r_ = min(r_, run == 0u ? 3u : 4u);     /* acc: at most 4 new bytes per put */
+                            }
+                            go = r_ != 0u;
+                            if ((uint32_t)__builtin_popcountll(__ballot(go)) < K2_LITMIN) break;
+                            if (go) {
+                                K2_SITE(9);
+                                curw |= ((1u << r_) - 1u) << (p & 31u);
+                                const uint32_t lo_ = ln_sel4(W, x_ >> 2), hi_ = ln_sel4(W, (x_ >> 2) + 1u);
+                                const uint32_t by_ = __builtin_amdgcn_alignbit(hi_, lo_, 8u * (x_ & 3u)) &
+                                                     (r_ == 4u ? 0xFFFFFFFFu : (1u << (8u * r_)) - 1u);
+                                const bool first_ = run == 0u;
+                                hx = first_ ? 4u * fw + accn : hx;
+                                K2_PUT(first_ ? (uint64_t)by_ << 8 : (uint64_t)by_, first_ ? r_ + 1u : r_);
+                                o += r_;
+                                run += r_;
+                                if (run == LZF_MAX_LIT) { K2_PATCH(hx, LZF_MAX_LIT - 1u); run = 0u; o++; }
+                                p += r_;
+                                if ((p & 31u) == 0u) {
+                                    K2_FLUSH_TO(cw);
+                                    K2_RING(cw) = curw;
+                                    cw++;
+                                    curw = 0u;
+                                }
+                            }
+                        }
+                    }
+#else
                     if ((uint32_t)__builtin_popcountll(__ballot(true)) >= K2_LITMIN)
 #pragma unroll
                     for (uint32_t e_ = 0; e_ < K2_LITX; e_++) {
@@ -1191,6 +1248,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                             }
                         }
                     }
+#endif  /* K2_LITB */
 #endif
                 }
             } else {
