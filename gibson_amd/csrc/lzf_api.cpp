@@ -256,19 +256,20 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s, ScratchUser who)
 /* smallest batch the lane / table generations take (LZF_GPU_LANE_MIN
  * overrides): below it window64's one wave per value finishes first, since
  * the parse's time has a floor of one whole value's parse per lane.
- * tools/crossover.py, table generation vs window64 (ms): 8 KiB text 11.6 vs
- * 5.8 at 16 K values, 15.5 vs 22.4 at 64 K; 16 KiB mixed 44.0 vs 41.4 at
- * 64 K, 54.5 vs 82.3 at 128 K; 64 KiB text 94.2 vs 50.5 at 16 K, 116.8 vs
- * 197.3 at 64 K (profiles/r02/crossover_table.txt).  The 4 KiB lane small
- * class: near 160 K values (round 1). */
+ * tools/crossover.py, round 4, the routed generations (stream cand + lane
+ * parse up to 16 KiB, table above) vs window64, compress ms
+ * (profiles/r04/xo_*.txt): json 4 KiB 7.02 vs 6.61 at 96 K values, 7.71 vs
+ * 8.78 at 128 K; text 8 KiB 11.21 vs 11.31 at 32 K; mixed 16 KiB 24.80 vs
+ * 20.07 at 32 K, 26.37 vs 29.86 at 48 K; text 64 KiB 77.22 vs 69.47 at 24 K,
+ * 80.45 vs 92.62 at 32 K. */
 uint32_t lane_min_count(uint32_t max_len)
 {
     const char *e = getenv("LZF_GPU_LANE_MIN");
     if (e) return (uint32_t)strtoul(e, nullptr, 10);
-    if (max_len <= 4096u) return 163840u;
-    if (max_len <= 8192u) return 40960u;
-    if (max_len <= 16384u) return 81920u;
-    return 32768u;
+    if (max_len <= 4096u) return 114688u;
+    if (max_len <= 8192u) return 32768u;
+    if (max_len <= 16384u) return 45056u;
+    return 28672u;
 }
 
 hipError_t launch_compress(const LzfBatch &b, hipStream_t s)

@@ -42,7 +42,9 @@ def t(count, gen):
     return sorted(ts)[1] * 1e3
 
 
-for count in (1 << 10, 1 << 12, 1 << 14, 1 << 16, 1 << 17, 1 << 18, 1 << 19, 1 << 20):
+counts = [int(c) for c in os.environ["XO_COUNTS"].split(",")] if os.environ.get("XO_COUNTS") else \
+    [1 << 10, 1 << 12, 1 << 14, 1 << 16, 1 << 17, 1 << 18, 1 << 19, 1 << 20]
+for count in counts:
     if count > N:
         break
     print(f"{count:8d} values: lane {t(count, 'lane'):8.2f} ms   window {t(count, 'window'):8.2f} ms", flush=True)

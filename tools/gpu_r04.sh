@@ -64,6 +64,10 @@ for st in "$@"; do
             IFS=: read -r _ k nn c <<< "$st"
             timeout -k 10 300 python -u tools/dec_tstat.py $k $nn $c gibson_amd/liblzf_hip_time.so > $O/tstat_${k}_${nn}.txt 2>&1 || exit 1
             grep -v amdgpu.ids $O/tstat_${k}_${nn}.txt ;;
+    xo:*)   # xo:<kind>:<n>:<max count>:<counts, comma-separated> -- lane route vs window64 by batch size
+            IFS=: read -r _ k nn c cs <<< "$st"
+            XO_COUNTS=$cs timeout -k 10 600 python -u tools/crossover.py $k $nn $c > $O/xo_${k}_${nn}.txt 2>&1 || exit 1
+            grep -v amdgpu.ids $O/xo_${k}_${nn}.txt ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
