@@ -157,6 +157,28 @@ def test_batch_decompress_golden(golden, oracle):
     assert not bad, f"{len(bad)} mismatches, first: {bad[:5]}"
 
 
+def test_batch_decompress_golden_per_window(golden, oracle):
+    # the decoder instance follows the batch's largest out_len (tokpar64 per
+    # window of 256 B .. 4 KiB, the pipe past that): the golden decoder
+    # corpus (valid, tight, truncated, corrupted, random streams) split into
+    # one batch per window size, so every instance meets the error cases
+    from tests.gpu_batch import gpu_decompress
+    from tests.test_oracle import decoder_cases
+    buckets = {}
+    for c, s in decoder_cases(golden, oracle):
+        w = 256
+        while w < c["out_len"] and w < 8192:
+            w <<= 1
+        buckets.setdefault(w, []).append((c, s))
+    assert len(buckets) >= 4, sorted(buckets)
+    for w, cases in sorted(buckets.items()):
+        res = gpu_decompress([s for _, s in cases], [c["out_len"] for c, _ in cases])
+        bad = [(c.get("tag"), c["result"], c["errno"], len(out) if out else 0, e)
+               for (c, s), (out, e) in zip(cases, res)
+               if (len(out) if out else 0) != c["result"] or e != c["errno"] or (out and sha16(out) != c["out_sha"])]
+        assert not bad, f"window {w}: {len(bad)} mismatches of {len(cases)}, first: {bad[:5]}"
+
+
 def test_decoded_size_prepass_golden(golden, oracle):
     # the pre-pass (lzf_dsize.hip) against the reference's decode length and
     # errno on the whole golden decoder corpus: valid, tight, truncated at
