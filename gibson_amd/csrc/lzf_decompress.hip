@@ -159,67 +159,17 @@ __device__ __forceinline__ void cd_stage(uint8_t *inr, const uint8_t *src, uint3
     }
 }
 
-/* step 1: lane l gets the round-relative start of token l (CD_ROUND: none);
- * nbase = the input offset after the round's last token */
-__device__ __forceinline__ uint32_t cd_discover(const uint8_t *inr, uint32_t imask, uint8_t *tokpos,
-                                                uint32_t base, uint32_t in_len, uint32_t lane, uint32_t &nbase)
-{
-    const uint32_t pa = 2u * lane, pb = pa + 1u;
-    const uint32_t ca = inr[(base + pa) & imask], cb = inr[(base + pb) & imask];
-    const uint32_t ta = cd_tsz(ca), tb = cd_tsz(cb);
-    (void)tokpos;
-    /* jump tables J0..J5 over the round's 128 positions packed two per lane
-     * as bytes (bits 0-7: position 2l, 8-15: 2l + 1).  Leaving the round is
-     * 255, which reads lane 63's odd half -- position 127, whose token always
-     * leaves the round -- so 255 maps to itself at every level and no level
-     * tests for it.  A round holds <= 64 tokens (each takes >= 2 bytes):
-     * lane l finds the start of token l with six doubling levels */
-    uint32_t PJ[6];
-    {
-        const uint32_t ipa = base + pa;
-        uint32_t na = pa + ta, nb = pb + tb;
-        if (ipa + ta >= in_len || na >= CD_ROUND) na = 255u;
-        if (ipa + 1u + tb >= in_len || nb >= CD_ROUND) nb = 255u;
-        PJ[0] = na | (nb << 8);
-    }
-#pragma unroll
-    for (uint32_t k = 1; k < 6u; k++) {
-        const uint32_t P = PJ[k - 1u], ja = P & 0xFFu, jb = (P >> 8) & 0xFFu;
-        const uint32_t wa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((ja & 0x7Eu) << 1), (int)P);
-        const uint32_t wb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((jb & 0x7Eu) << 1), (int)P);
-        PJ[k] = ((wa >> ((ja & 1u) << 3)) & 0xFFu) | (((wb >> ((jb & 1u) << 3)) & 0xFFu) << 8);
-    }
-    uint32_t x = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 6u; b++) {
-        const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((x & 0x7Eu) << 1), (int)PJ[b]);
-        const uint32_t y = (w >> ((x & 1u) << 3)) & 0xFFu;
-        x = ((lane >> b) & 1u) ? y : x;
-    }
-    if (x >= CD_ROUND) x = CD_ROUND;
-    /* the next round starts after the last token */
-    const bool tok = x < CD_ROUND;
-    const uint32_t ntok = (uint32_t)__builtin_popcountll(cd_ballot(tok));
-    const uint32_t c = inr[(base + (tok ? x : 0u)) & imask];
-    nbase = base + cd_rl(x + cd_tsz(c), ntok - 1u);
-    return x;
-}
-
-/* step 1 with the jump table in LDS (the pipe; CD_JLDS): jt holds 256 bytes,
+/* step 1: lane l gets the round-relative start of token l (CD_ROUND: none).
+ * The jump table lives in LDS: jt holds 256 bytes,
  * J(p) for the round's positions p < 128 and 255 ("leaves the round") at
  * [128, 256), so a jump is one ds_read_u8 at the entry itself.  Level b's
  * table is read at J_b(p) to make J_{b+1} and at the lane's rank walk x, and
  * overwritten in place: one wave's LDS operations execute in order, so every
  * lane's reads of level b precede the write.  The rank walk applies level b
  * as the table reaches it (the levels are powers of one map, so they commute):
- * four LDS operations per level against two ds_bpermute and their byte
- * extraction per table level plus one per rank level. */
-#ifndef CD_JLDS
-#define CD_JLDS 1
-#endif
-#ifndef CD_TSZT
-#define CD_TSZT 1
-#endif
+ * four LDS operations per level (round 3 held the tables in registers, two
+ * per lane: two ds_bpermute and their byte extraction per table level plus
+ * one per rank level). */
 #ifndef CD_PREF
 #define CD_PREF 1
 #endif
@@ -230,20 +180,20 @@ __device__ __forceinline__ uint32_t cd_discover(const uint8_t *inr, uint32_t ima
 #ifndef CD_CPRIO
 #define CD_CPRIO 1
 #endif
-/* CD_TSZT: token sizes from a 256-byte LDS table, tszt[c] = cd_tsz(c), at jt + 256 */
-__device__ __forceinline__ void cd_tszt_init(uint8_t *jt, uint32_t lane)
+/* the jump table's 255s above position 127, and token sizes from a 256-byte
+ * table, tszt[c] = cd_tsz(c), at jt + 256 (one LDS read instead of six VALU) */
+__device__ __forceinline__ void cd_jt_init(uint8_t *jt, uint32_t lane)
 {
-    if (CD_TSZT) {
-        const uint32_t c = 4u * lane;
-        *(uint32_t *)(jt + 256u + c) = cd_tsz(c) | (cd_tsz(c + 1u) << 8) | (cd_tsz(c + 2u) << 16) | (cd_tsz(c + 3u) << 24);
-    }
+    *(uint16_t *)(jt + CD_ROUND + 2u * lane) = 0xFFFFu;
+    const uint32_t c = 4u * lane;
+    *(uint32_t *)(jt + 256u + c) = cd_tsz(c) | (cd_tsz(c + 1u) << 8) | (cd_tsz(c + 2u) << 16) | (cd_tsz(c + 3u) << 24);
 }
 __device__ __forceinline__ uint32_t cd_discover_lds(const uint8_t *inr, uint32_t imask, uint8_t *jt, uint32_t base,
                                                     uint32_t in_len, uint32_t lane)
 {
     const uint32_t pa = 2u * lane, pb = pa + 1u;
     const uint32_t ca = inr[(base + pa) & imask], cb = inr[(base + pb) & imask];
-    const uint32_t ta = CD_TSZT ? jt[256u + ca] : cd_tsz(ca), tb = CD_TSZT ? jt[256u + cb] : cd_tsz(cb);
+    const uint32_t ta = jt[256u + ca], tb = jt[256u + cb];
     /* J0 = the next token's start: any entry >= 128 leaves the round (the
      * table holds 255 there, so its first jump gives 255); away from the
      * stream's end no token crosses in_len, so only near it are entries
@@ -274,7 +224,7 @@ __device__ __forceinline__ uint32_t cd_discover_lds(const uint8_t *inr, uint32_t
 
 /* steps 2-3 for lane l's token: its output offset within the round (rel),
  * the owner info of its output bytes (tinfo: literal -> input ring index
- * o + tinfo, flagged in bit 31; back-ref -> distance), the round's output
+ * o - tinfo, flagged in bit 31; back-ref -> distance), the round's output
  * bytes, and errno of the first failing token (0: none) */
 #ifndef CD_PER_RATIO
 #define CD_PER_RATIO 4u
@@ -304,7 +254,10 @@ __device__ __forceinline__ CdRound cd_decode(const uint8_t *inr, uint32_t imask,
     CdRound r;
     r.rel = incl - ol;
     const uint32_t Ot = O + r.rel;                      /* output offset of my token */
-    r.tinfo = lit ? (((lsrc - Ot) & 0x7FFFFFFFu) | 0x80000000u) : back;
+    /* literal: Ot - lsrc, so the consumer's o - tinfo is the input offset
+     * of output byte o for both kinds (the flag, 2^31, leaves the ring's
+     * low bits alone) */
+    r.tinfo = lit ? (((Ot - lsrc) & 0x7FFFFFFFu) | 0x80000000u) : back;
     r.total = cd_rl(incl, 63u);
     /* the round's last token (lane ntok - 1: tokens fill the low lanes) ends the round */
     r.ntok = (uint32_t)__builtin_popcountll(cd_ballot(tok));
@@ -377,9 +330,6 @@ __device__ __forceinline__ void cd_flush(const uint8_t *lds, uint32_t outr_off, 
 #ifndef CD_PERIOD
 #define CD_PERIOD 1
 #endif
-#ifndef CD_MARKNB
-#define CD_MARKNB 1
-#endif
 template <uint32_t IN_RING, bool PER = false>
 __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint32_t omask, uint32_t *mark,
                                              uint32_t sink_off, uint8_t *dst, uint32_t O, uint32_t total, bool tok,
@@ -394,12 +344,11 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
 #ifdef LZF_CD_ABLATE_OUTPUT           /* diagnostic builds only: time discovery alone */
     total = 0u;
 #endif
+    /* lanes without a token mark slot 64 (never read): their start lies 2^31 away */
+    const uint32_t Otm = tok ? Ot : Ot + 0x80000000u;
     for (uint32_t g = 0; g < total; g += CD_LANES) {
         const uint32_t gb = O + g;                     /* group's first output offset */
-        if (CD_MARKNB)       /* without a branch: other lanes mark slot 64 (never read) */
-            mark[tok && Ot - gb < CD_LANES ? Ot - gb : CD_LANES] = gb + 1u;
-        else if (tok && Ot - gb < CD_LANES)
-            mark[Ot - gb] = gb + 1u;
+        mark[min(Otm - gb, CD_LANES)] = gb + 1u;     /* without a branch */
         cd_fence();
         const bool mine = mark[lane] == gb + 1u;
         const uint64_t S = cd_ballot(mine);
@@ -425,8 +374,7 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
             }
         }
         /* the input ring lies right after the window */
-        const uint32_t li = IN_RING <= omask + 1u ? ((o + tInf) & imask) | (omask + 1u)
-                                                  : ((o + tInf) & imask) + (omask + 1u);
+        const uint32_t li = IN_RING <= omask + 1u ? (so & imask) | (omask + 1u) : (so & imask) + (omask + 1u);
         const uint32_t a = outr_off + ((li & lit) | ((so & omask) & ~lit));
         const uint32_t q = so - gb;
         const uint32_t b = lds[a];
@@ -440,7 +388,7 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
                 ent = __builtin_amdgcn_ds_bpermute(ent < 0 ? me : ent >> 8, ent);
             while (cd_ballot(ent >= 0));
         }
-        const bool live = g + lane < total;
+        const bool live = lane < total - g;
         lds[live ? outr_off + (o & omask) : sink_off] = (uint8_t)ent;
         cd_fence();
         {
@@ -547,7 +495,7 @@ __device__ __forceinline__ void cd_output_tok(uint8_t *inr, uint8_t *outr, uint8
         const bool ready = !done && (lit || e <= O || before == 0ull || endj <= s);
         if (ready) {
             if (lit) {
-                const uint32_t ri = (Ot + info) & (CD_IN_RINGP - 1u);
+                const uint32_t ri = (Ot - info) & (CD_IN_RINGP - 1u);
                 for (uint32_t c = 0; c < len; c += 16u)
                     cd_st(outr + Ot + c, cd_ld(inr + ri + c), len - c);
             } else {
@@ -596,13 +544,13 @@ template <uint32_t RING>
 __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, uint32_t out_ring)
 {
     __shared__ __attribute__((aligned(16))) uint8_t smem[CD_IN_RING1 + RING + CD_LANES * 5u +
-                                                         (CD_JLDS ? (CD_TSZT ? 512u : 256u) : 0u)];
+                                                         512u];   /* + jump and token-size tables */
     out_ring = RING;
     uint8_t *outr = smem;                              /* out_ring (power of two) */
     uint8_t *inr = outr + out_ring;                    /* CD_IN_RING1, right after the window (cd_output) */
     uint32_t *mark = (uint32_t *)(inr + CD_IN_RING1);  /* 64 token-start marks (group tags) */
     uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* the idle lanes' byte sink */
-    uint8_t *jt = tokpos + CD_LANES;                   /* CD_JLDS: the jump table */
+    uint8_t *jt = tokpos + CD_LANES;                   /* the jump table (+ token sizes) */
     const uint32_t imask = CD_IN_RING1 - 1u, omask = out_ring - 1u;
 
     const uint32_t lane = threadIdx.x;
@@ -616,10 +564,7 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
     const uint32_t avail = in_len ? in_len : 1u;
 
     mark[lane] = 0u;            /* group tags are >= 1 */
-    if (CD_JLDS) {
-        *(uint16_t *)(jt + CD_ROUND + 2u * lane) = 0xFFFFu;
-        cd_tszt_init(jt, lane);
-    }
+    cd_jt_init(jt, lane);
     uint32_t loaded = 0, base = 0, O = 0;
     uint32_t F = 0;             /* output [0, F) stored */
     int32_t err = 0;
@@ -627,9 +572,7 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
     while (first || base < in_len) {                     /* src/lzf_d.c:64, 146 */
         first = false;
         cd_stage<CD_IN_RING1>(inr, src, base, avail, loaded, lane);
-        uint32_t nb0;
-        const uint32_t x = CD_JLDS ? cd_discover_lds(inr, imask, jt, base, in_len, lane)
-                                   : cd_discover(inr, imask, tokpos, base, in_len, lane, nb0);
+        const uint32_t x = cd_discover_lds(inr, imask, jt, base, in_len, lane);
         const CdRound r = cd_decode(inr, imask, base, x, O, in_len, cap);
         if (r.err) {
             err = r.err;
@@ -677,19 +620,12 @@ __device__ __forceinline__ void cd_stage_pipe(uint8_t *inr, const uint8_t *src, 
 /* the pipe's window is always CD_OUT_MAX (values over 4 KiB), so its LDS is
  * static: the compiler folds the LDS base into every address (with dynamic
  * LDS it adds the base, 0, with one VALU per LDS address) */
-#ifndef CD_PIPE_STATIC
-#define CD_PIPE_STATIC 1
-#endif
 #define CD_PIPE_LDS (CD_IN_RINGP + 2u * sizeof(CdSlot) + 5u * CD_LANES + 16u + CD_OUT_MAX + \
-                     (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u) + (CD_JLDS ? (CD_TSZT ? 512u : 256u) : 0u))
+                     (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u) + 512u)   /* + jump and token-size tables */
 __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, uint32_t out_ring)
 {
-#if CD_PIPE_STATIC
     __shared__ __attribute__((aligned(16))) uint8_t smem[CD_PIPE_LDS];
     out_ring = CD_OUT_MAX;
-#else
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-#endif
     CdSlot *slot = (CdSlot *)smem;                     /* 2 */
     uint32_t *mark = (uint32_t *)(slot + 2);           /* the consumer's 64 token-start marks */
     uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* unused (was the removed walk's token starts) */
@@ -697,7 +633,7 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
     uint8_t *outr = sink + 16u;                        /* out_ring (power of two) */
     uint8_t *inr = outr + out_ring;                    /* CD_IN_RINGP, right after the window (cd_output);
                                                           CD_TOKOUT: + the mirror and 16 bytes */
-    uint8_t *jt = inr + CD_IN_RINGP + (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u);   /* CD_JLDS: the jump table */
+    uint8_t *jt = inr + CD_IN_RINGP + (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u);   /* the jump table (+ token sizes) */
     const uint32_t imask = CD_IN_RINGP - 1u, omask = out_ring - 1u;
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -717,10 +653,7 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
         const uint8_t *src = bt.in + bt.in_off[v];
         const uint32_t avail = in_len ? in_len : 1u;   /* a 0-length stream still reads one byte */
         uint32_t loaded = 0, base = 0, O = 0;
-        if (CD_JLDS) {
-            *(uint16_t *)(jt + CD_ROUND + 2u * lane) = 0xFFFFu;
-            cd_tszt_init(jt, lane);
-        }
+        cd_jt_init(jt, lane);
         /* CD_PREF: the input the next round needs is loaded at the start of
          * this round and written to the ring when the next round starts, so
          * its load latency is off the producer's chain (the synchronous stage
@@ -752,9 +685,7 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
                 if (px < pto) pv = cd_ld16(src + px, pto - px);
                 pend = true;
             }
-            uint32_t nb0;
-            const uint32_t x = CD_JLDS ? cd_discover_lds(inr, imask, jt, base, in_len, lane)
-                                       : cd_discover(inr, imask, tokpos, base, in_len, lane, nb0);
+            const uint32_t x = cd_discover_lds(inr, imask, jt, base, in_len, lane);
             const CdRound r = cd_decode(inr, imask, base, x, O, in_len, cap);
             const uint32_t ntok = r.ntok;
             const uint32_t total = r.total;
@@ -832,21 +763,9 @@ hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s)
 {
     uint32_t ring = 256u;
     while (ring < b.max_len && ring < CD_OUT_MAX) ring <<= 1;
-    hipError_t e;
     if (CD_PIPE && ring >= CD_PIPE_MIN_RING) {
-        /* CD_TOKOUT: + the input ring's mirror and 16 bytes past the window
-         * (a 16-byte read near its end) */
-        size_t lds = CD_IN_RINGP + 2u * sizeof(CdSlot) + 5u * CD_LANES + 16u + ring +
-                     (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u) + (CD_JLDS ? (CD_TSZT ? 512u : 256u) : 0u);
-        if (CD_PIPE_STATIC) {
-            if (ring != CD_OUT_MAX) return hipErrorInvalidValue;
-            lds = 0;
-        } else {
-            e = hipFuncSetAttribute((const void *)lzf_decompress_pipe_kernel,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
-        }
-        hipLaunchKernelGGL(lzf_decompress_pipe_kernel, dim3(b.count), dim3(2u * CD_LANES), lds, s, b, ring);
+        if (ring != CD_OUT_MAX) return hipErrorInvalidValue;   /* static LDS for the 8 KiB window */
+        hipLaunchKernelGGL(lzf_decompress_pipe_kernel, dim3(b.count), dim3(2u * CD_LANES), 0, s, b, ring);
     } else {
         /* LDS: the input ring, the window, the 64 marks and token starts */
         switch (ring) {
