@@ -348,9 +348,13 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
     const uint32_t Otm = tok ? Ot : Ot + 0x80000000u;
     for (uint32_t g = 0; g < total; g += CD_LANES) {
         const uint32_t gb = O + g;                     /* group's first output offset */
-        mark[min(Otm - gb, CD_LANES)] = gb + 1u;     /* without a branch */
+        const uint32_t o = gb + lane;
+        /* a start mark holds the token's own start, so it matches only in its
+         * group (no per-group tag; position 0, the unwritten marks' 0, always
+         * starts a token) */
+        mark[min(Otm - gb, CD_LANES)] = Otm;          /* without a branch */
         cd_fence();
-        const bool mine = mark[lane] == gb + 1u;
+        const bool mine = mark[lane] == o;
         const uint64_t S = cd_ballot(mine);
         const uint32_t le = __builtin_amdgcn_mbcnt_hi((uint32_t)(S >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)S, 0u)) +
@@ -358,8 +362,7 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
         const uint32_t k = tbase + le - 1u;
         tbase += (uint32_t)__builtin_popcountll(S);
         const uint32_t tInf = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)tinfo);
-        const uint32_t o = gb + lane;
-        const uint32_t lit = (uint32_t)((int32_t)tInf >> 31);
+        const bool lit = (int32_t)tInf < 0;
         uint32_t so = o - tInf;
         if (PER) {                                     /* a round the producer flagged */
             const uint32_t ot = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)Ot);
@@ -375,7 +378,7 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
         }
         /* the input ring lies right after the window */
         const uint32_t li = IN_RING <= omask + 1u ? (so & imask) | (omask + 1u) : (so & imask) + (omask + 1u);
-        const uint32_t a = outr_off + ((li & lit) | ((so & omask) & ~lit));
+        const uint32_t a = outr_off + (lit ? li : so & omask);
         const uint32_t q = so - gb;
         const uint32_t b = lds[a];
         /* resolved: bit 31 | the byte; pending: the source lane's ds_bpermute
@@ -389,7 +392,7 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
             while (cd_ballot(ent >= 0));
         }
         const bool live = lane < total - g;
-        lds[live ? outr_off + (o & omask) : sink_off] = (uint8_t)ent;
+        lds[outr_off + (live ? o & omask : sink_off - outr_off)] = (uint8_t)ent;   /* the sink lies past the window */
         cd_fence();
         {
             const uint32_t done = g + CD_LANES <= total ? gb + CD_LANES : O + total;
@@ -628,12 +631,12 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
     out_ring = CD_OUT_MAX;
     CdSlot *slot = (CdSlot *)smem;                     /* 2 */
     uint32_t *mark = (uint32_t *)(slot + 2);           /* the consumer's 64 token-start marks */
-    uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* unused (was the removed walk's token starts) */
-    uint8_t *sink = tokpos + CD_LANES;                 /* the consumer's idle-lane byte sink */
-    uint8_t *outr = sink + 16u;                        /* out_ring (power of two) */
+    uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* slot 64 of the marks (never read) */
+    uint8_t *outr = tokpos + CD_LANES;                 /* out_ring (power of two) */
     uint8_t *inr = outr + out_ring;                    /* CD_IN_RINGP, right after the window (cd_output);
                                                           CD_TOKOUT: + the mirror and 16 bytes */
     uint8_t *jt = inr + CD_IN_RINGP + (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u);   /* the jump table (+ token sizes) */
+    uint8_t *sink = jt + 512u;                         /* the consumer's idle-lane byte sink, past the window */
     const uint32_t imask = CD_IN_RINGP - 1u, omask = out_ring - 1u;
 
     const uint32_t lane = threadIdx.x & 63u;
