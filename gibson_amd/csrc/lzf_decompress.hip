@@ -551,9 +551,9 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
     out_ring = RING;
     uint8_t *outr = smem;                              /* out_ring (power of two) */
     uint8_t *inr = outr + out_ring;                    /* CD_IN_RING1, right after the window (cd_output) */
-    uint32_t *mark = (uint32_t *)(inr + CD_IN_RING1);  /* 64 token-start marks (group tags) */
-    uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* the idle lanes' byte sink */
-    uint8_t *jt = tokpos + CD_LANES;                   /* the jump table (+ token sizes) */
+    uint32_t *mark = (uint32_t *)(inr + CD_IN_RING1);  /* 64 token-start marks */
+    uint8_t *sink = (uint8_t *)(mark + CD_LANES);      /* the idle lanes' byte sink (and mark slot 64; both write-only) */
+    uint8_t *jt = sink + CD_LANES;                     /* the jump table (+ token sizes) */
     const uint32_t imask = CD_IN_RING1 - 1u, omask = out_ring - 1u;
 
     const uint32_t lane = threadIdx.x;
@@ -581,7 +581,7 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
             err = r.err;
             break;
         }
-        cd_output<CD_IN_RING1>(smem, 0u, omask, mark, (uint32_t)(tokpos - smem), dst, O, r.total,
+        cd_output<CD_IN_RING1>(smem, 0u, omask, mark, (uint32_t)(sink - smem), dst, O, r.total,
                                x < CD_ROUND, O + r.rel, r.tinfo, lane, F);
         O += r.total;
         base = r.nbase;
@@ -631,8 +631,8 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
     out_ring = CD_OUT_MAX;
     CdSlot *slot = (CdSlot *)smem;                     /* 2 */
     uint32_t *mark = (uint32_t *)(slot + 2);           /* the consumer's 64 token-start marks */
-    uint8_t *tokpos = (uint8_t *)(mark + CD_LANES);    /* slot 64 of the marks (never read) */
-    uint8_t *outr = tokpos + CD_LANES;                 /* out_ring (power of two) */
+    uint8_t *mark64 = (uint8_t *)(mark + CD_LANES);    /* mark slot 64 (write-only) and spare */
+    uint8_t *outr = mark64 + CD_LANES;                 /* out_ring (power of two) */
     uint8_t *inr = outr + out_ring;                    /* CD_IN_RINGP, right after the window (cd_output);
                                                           CD_TOKOUT: + the mirror and 16 bytes */
     uint8_t *jt = inr + CD_IN_RINGP + (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u);   /* the jump table (+ token sizes) */
