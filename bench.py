@@ -483,14 +483,16 @@ def main_decompress(a, world, rank, dev, cfg_idx, kind, seed, n, count):
             "warmup": a.warmup,
             "ms_per_step": round(sec_per_step * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if a.total else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": f"{count // (1 << 20)}M x {n // 1024} KiB pre-compressed blocks per GPU, "
-                            f"decompress only (BASELINE configs[3])" if count >= (1 << 20) else
-                            f"{count} x {n} B pre-compressed blocks per GPU, decompress only",
+                "workload": (f"{a.total} x {n // 1024} KiB pre-compressed blocks over all ranks, decompress only"
+                             if a.total else
+                             f"{count // (1 << 20)}M x {n // 1024} KiB pre-compressed blocks per GPU, "
+                             f"decompress only (BASELINE configs[3])" if count >= (1 << 20) else
+                             f"{count} x {n} B pre-compressed blocks per GPU, decompress only"),
                 "baseline_config": 3,
                 "values_per_gpu": count,
                 "value_bytes": n,

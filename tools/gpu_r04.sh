@@ -68,6 +68,11 @@ for st in "$@"; do
             IFS=: read -r _ k nn c cs <<< "$st"
             XO_COUNTS=$cs timeout -k 10 600 python -u tools/crossover.py $k $nn $c > $O/xo_${k}_${nn}.txt 2>&1 || exit 1
             grep -v amdgpu.ids $O/xo_${k}_${nn}.txt ;;
+    gpus2)  # the N-rank path rehearsed: two ranks on the one device, gloo barrier/reductions
+            LZF_BENCH_BACKEND=gloo LZF_BENCH_SHARE_GPU=1 timeout -k 10 600 python bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu > $O/gpus2.json 2> $O/gpus2.err || exit 1
+            tail -1 $O/gpus2.json | cut -c1-400
+            LZF_BENCH_BACKEND=gloo LZF_BENCH_SHARE_GPU=1 timeout -k 10 600 python bench.py --gpus 2 --mode decompress --total 4194304 --steps 2 --warmup 1 --no-cpu > $O/gpus2_dec.json 2> $O/gpus2_dec.err || exit 1
+            tail -1 $O/gpus2_dec.json | cut -c1-400 ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
