@@ -182,18 +182,21 @@ __device__ __forceinline__ void cd_stage(uint8_t *inr, const uint8_t *src, uint3
 #endif
 /* the jump table's 255s above position 127, and token sizes from a 256-byte
  * table, tszt[c] = cd_tsz(c), at jt + 256 (one LDS read instead of six VALU) */
+template <bool TSZT = true>
 __device__ __forceinline__ void cd_jt_init(uint8_t *jt, uint32_t lane)
 {
     *(uint16_t *)(jt + CD_ROUND + 2u * lane) = 0xFFFFu;
     const uint32_t c = 4u * lane;
-    *(uint32_t *)(jt + 256u + c) = cd_tsz(c) | (cd_tsz(c + 1u) << 8) | (cd_tsz(c + 2u) << 16) | (cd_tsz(c + 3u) << 24);
+    if (TSZT)
+        *(uint32_t *)(jt + 256u + c) = cd_tsz(c) | (cd_tsz(c + 1u) << 8) | (cd_tsz(c + 2u) << 16) | (cd_tsz(c + 3u) << 24);
 }
+template <bool TSZT = true>
 __device__ __forceinline__ uint32_t cd_discover_lds(const uint8_t *inr, uint32_t imask, uint8_t *jt, uint32_t base,
                                                     uint32_t in_len, uint32_t lane)
 {
     const uint32_t pa = 2u * lane, pb = pa + 1u;
     const uint32_t ca = inr[(base + pa) & imask], cb = inr[(base + pb) & imask];
-    const uint32_t ta = jt[256u + ca], tb = jt[256u + cb];
+    const uint32_t ta = TSZT ? jt[256u + ca] : cd_tsz(ca), tb = TSZT ? jt[256u + cb] : cd_tsz(cb);
     /* J0 = the next token's start: any entry >= 128 leaves the round (the
      * table holds 255 there, so its first jump gives 255); away from the
      * stream's end no token crosses in_len, so only near it are entries
@@ -340,8 +343,8 @@ __device__ __forceinline__ void cd_flush(const uint8_t *lds, uint32_t outr_off, 
 #ifndef CD_MARKAHEAD_PIPE           /* the pipe's consumer */
 #define CD_MARKAHEAD_PIPE 0
 #endif
-template <uint32_t IN_RING, bool PER = false, bool MA = CD_MARKAHEAD>
-__device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint32_t omask, uint32_t *mark,
+template <uint32_t IN_RING, bool PER = false, bool MA = CD_MARKAHEAD, typename MT = uint32_t>
+__device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint32_t omask, MT *mark,
                                              uint32_t sink_off, uint8_t *dst, uint32_t O, uint32_t total, bool tok,
                                              uint32_t Ot, uint32_t tinfo, uint32_t lane, uint32_t &F)
 {
@@ -361,7 +364,7 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
      * starts a token) */
     uint32_t m = 0u;
     if (MA && total) {
-        mark[min(Otm - O, CD_LANES)] = Otm;           /* without a branch */
+        mark[min(Otm - O, CD_LANES)] = (MT)Otm;       /* without a branch */
         cd_fence();
         m = mark[lane];
     }
@@ -369,11 +372,11 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
         const uint32_t gb = O + g;                     /* group's first output offset */
         const uint32_t o = gb + lane;
         if (!MA) {
-            mark[min(Otm - gb, CD_LANES)] = Otm;
+            mark[min(Otm - gb, CD_LANES)] = (MT)Otm;
             cd_fence();
             m = mark[lane];
         }
-        const bool mine = m == o;
+        const bool mine = (MT)m == (MT)o;   /* 16-bit marks: a stream's output stays below 65536 */
         const uint64_t S = cd_ballot(mine);
         const uint32_t le = __builtin_amdgcn_mbcnt_hi((uint32_t)(S >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)S, 0u)) +
@@ -386,7 +389,7 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
              * chain (they depend on nothing it writes; a group past the
              * round marks slot 64 only: no token starts there) */
             cd_fence();
-            mark[min(Otm - (gb + CD_LANES), CD_LANES)] = Otm;
+            mark[min(Otm - (gb + CD_LANES), CD_LANES)] = (MT)Otm;
             cd_fence();
             m = mark[lane];
         }
@@ -570,18 +573,34 @@ __device__ __forceinline__ bool cd_refused(const LzfBatch &bt, uint32_t v, uint3
     return true;
 }
 
+/* CD_TP_SMALL: windows up to 4 KiB (the output stays below 65536, so 16-bit
+ * start marks match only in their group) keep 16-bit marks and compute token
+ * sizes instead of reading the 256-byte table: 5008 bytes of LDS for a 4 KiB
+ * window, 32 streams per CU (the wave limit) instead of 30 */
+#ifndef CD_TP_SMALL
+#define CD_TP_SMALL 1
+#endif
+#ifndef CD_TP_TSZT
+#define CD_TP_TSZT 0
+#endif
+template <bool B> struct CdMark { typedef uint32_t T; };
+template <> struct CdMark<true> { typedef uint16_t T; };
 /* one instance per window size, with static LDS (as the pipe) */
 template <uint32_t RING>
 __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, uint32_t out_ring)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[CD_IN_RING1 + RING + CD_LANES * 5u +
-                                                         512u];   /* + jump and token-size tables */
+    constexpr bool SMALL = CD_TP_SMALL && RING <= 4096u;
+    constexpr bool TSZT = !SMALL || CD_TP_TSZT;
+    typedef typename CdMark<SMALL>::T MT;
+    constexpr uint32_t MARKB = SMALL ? 2u * CD_LANES + 16u : 5u * CD_LANES;   /* marks + slot 64 and the sink */
+    __shared__ __attribute__((aligned(16))) uint8_t smem[CD_IN_RING1 + RING + MARKB +
+                                                         (TSZT ? 512u : 256u)];   /* + jump (and token-size) tables */
     out_ring = RING;
     uint8_t *outr = smem;                              /* out_ring (power of two) */
     uint8_t *inr = outr + out_ring;                    /* CD_IN_RING1, right after the window (cd_output) */
-    uint32_t *mark = (uint32_t *)(inr + CD_IN_RING1);  /* 64 token-start marks */
+    MT *mark = (MT *)(inr + CD_IN_RING1);              /* 64 token-start marks */
     uint8_t *sink = (uint8_t *)(mark + CD_LANES);      /* the idle lanes' byte sink (and mark slot 64; both write-only) */
-    uint8_t *jt = sink + CD_LANES;                     /* the jump table (+ token sizes) */
+    uint8_t *jt = inr + CD_IN_RING1 + MARKB;           /* the jump table (+ token sizes) */
     const uint32_t imask = CD_IN_RING1 - 1u, omask = out_ring - 1u;
 
     const uint32_t lane = threadIdx.x;
@@ -594,8 +613,8 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
     /* as the reference, a 0-length stream still reads its first control byte */
     const uint32_t avail = in_len ? in_len : 1u;
 
-    mark[lane] = 0u;            /* group tags are >= 1 */
-    cd_jt_init(jt, lane);
+    mark[lane] = 0u;            /* position 0 always starts a token */
+    cd_jt_init<TSZT>(jt, lane);
     uint32_t loaded = 0, base = 0, O = 0;
     uint32_t F = 0;             /* output [0, F) stored */
     int32_t err = 0;
@@ -603,13 +622,13 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
     while (first || base < in_len) {                     /* src/lzf_d.c:64, 146 */
         first = false;
         cd_stage<CD_IN_RING1>(inr, src, base, avail, loaded, lane);
-        const uint32_t x = cd_discover_lds(inr, imask, jt, base, in_len, lane);
+        const uint32_t x = cd_discover_lds<TSZT>(inr, imask, jt, base, in_len, lane);
         const CdRound r = cd_decode(inr, imask, base, x, O, in_len, cap);
         if (r.err) {
             err = r.err;
             break;
         }
-        cd_output<CD_IN_RING1>(smem, 0u, omask, mark, (uint32_t)(sink - smem), dst, O, r.total,
+        cd_output<CD_IN_RING1, false, CD_MARKAHEAD, MT>(smem, 0u, omask, mark, (uint32_t)(sink - smem), dst, O, r.total,
                                x < CD_ROUND, O + r.rel, r.tinfo, lane, F);
         O += r.total;
         base = r.nbase;
