@@ -29,5 +29,11 @@ from .lzf import (  # noqa: F401
     synth_fill,
     host_compress_batch,
     host_decompress_batch,
+    host_register,
+    host_unregister,
+    device_plan,
+    host_last_spread,
+    host_split,
+    parse_device_list,
     kv_frame,
 )

@@ -1,19 +1,15 @@
 /*
- * lzf_api.cpp -- the C-ABI of liblzf_hip.so.
+ * lzf_api.cpp -- the device side of liblzf_hip.so's C-ABI.
  *
- * Exports the drop-in pair of include/lzf.h (replacing src/lzf_c.c:98 and
- * src/lzf_d.c:55 behind the prototypes of src/lzf.h:76-78, 95-97) and the
- * batched device API of include/lzf_gpu.h.  There is no CPU codec in this
- * library: every call runs the HIP kernels.  Failures never abort (a server
- * must survive a transient HIP error): when no gfx950 device is usable or a
- * HIP call fails, lzf_compress returns 0 (the caller stores the value plain,
- * src/query.c:393), lzf_decompress returns 0 with errno EIO, and the batch
- * calls return a negative LZF_GPU_E* code (LZF_GPU_ENODEV without a device).
- *
- * Single calls are batches of one.  Each calling thread owns a context
- * (stream, device buffers, pinned staging), created lazily on the device
- * named by LZF_GPU_DEVICE (default 0); the caller's current device is
- * restored before returning, so Gibson's event loop never has to touch HIP.
+ * The kernel routing (which generation compresses a batch, which decoder
+ * decodes it), the per-device compress scratch and the LDS lane-order
+ * self-check, and the device-pointer calls of include/lzf_gpu.h.  The
+ * host-memory calls -- the drop-in pair of include/lzf.h (src/lzf.h:76-78,
+ * 95-97) and the lzf_host_* batches -- are in lzf_host.cpp and launch
+ * through lzf_route_compress / lzf_route_decompress below.  There is no CPU
+ * codec in this library: every call runs the HIP kernels.  Failures never
+ * abort (a server must survive a transient HIP error): the batch calls
+ * return a negative LZF_GPU_E* code (LZF_GPU_ENODEV without a device).
  */
 #include <errno.h>
 #include <stdio.h>
@@ -336,13 +332,6 @@ hipError_t launch_decompress(const LzfBatch &b, hipStream_t s)
     }
 }
 
-/* Library failures inside the host-memory paths are thrown as LzfFail and
- * turned into an LZF_GPU_E* code at the C boundary (never abort: a transient
- * HIP error must not take the server down). */
-struct LzfFail {
-    int code;
-};
-
 int code_of(hipError_t e)
 {
     if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return LZF_GPU_ENOMEM;
@@ -350,454 +339,22 @@ int code_of(hipError_t e)
     return LZF_GPU_ELAUNCH;
 }
 
-void check(hipError_t e, const char *what)
-{
-    if (e == hipSuccess) return;
-    static bool said = false;
-    if (!said) {
-        said = true;
-        fprintf(stderr, "liblzf_hip: %s failed: %s\n", what, hipGetErrorString(e));
-    }
-    (void)hipGetLastError();
-    throw LzfFail{code_of(e)};
-}
-
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev)
-    {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) {
-            check(hipSetDevice(dev), "hipSetDevice");
-        }
-    }
-    ~DeviceGuard()
-    {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-    }
-};
-
-/* Growable device / pinned buffers of one thread. */
-struct Buf {
-    void *p = nullptr;
-    size_t cap = 0;
-    bool pinned = false;
-    void *get(size_t need)
-    {
-        if (need == 0) need = 1;
-        if (need <= cap) return p;
-        size_t want = need + need / 4 + 256;
-        if (p) { pinned ? (void)hipHostFree(p) : (void)hipFree(p); }
-        p = nullptr;
-        cap = 0;
-        hipError_t e = pinned ? hipHostMalloc(&p, want, hipHostMallocDefault) : hipMalloc(&p, want);
-        if (e != hipSuccess) {
-            p = nullptr;
-            check(e, pinned ? "hipHostMalloc" : "hipMalloc");
-        }
-        cap = want;
-        return p;
-    }
-    void release()
-    {
-        if (p) { pinned ? (void)hipHostFree(p) : (void)hipFree(p); }
-        p = nullptr;
-        cap = 0;
-    }
-};
-
-struct Meta {               /* one value's descriptor, packed for one copy */
-    uint64_t in_off, out_off;
-    uint32_t in_len, out_cap, out_len;
-    int32_t err;
-};
-
-/* One stage of the chunked host pipeline: its own stream, pinned and device
- * buffers, and the chunk it holds until the results are copied out. */
-struct Slot {
-    hipStream_t stream = nullptr;
-    hipEvent_t done = nullptr;
-    Buf d_in, d_out, d_meta;
-    Buf h_in{nullptr, 0, true}, h_out{nullptr, 0, true}, h_meta{nullptr, 0, true};
-    uint32_t first = 0, count = 0;
-    bool busy = false;
-};
-
-struct Ctx {
-    int dev = 0;
-    bool ok = false;
-    hipStream_t stream = nullptr;
-    Buf d_in, d_out, d_meta;
-    Buf h_in{nullptr, 0, true}, h_out{nullptr, 0, true}, h_meta{nullptr, 0, true};
-    Slot slot[2];
-    Ctx()
-    {
-        const char *e = getenv("LZF_GPU_DEVICE");
-        dev = e ? atoi(e) : 0;
-        int n = 0;
-        if (hipGetDeviceCount(&n) != hipSuccess || dev < 0 || dev >= n || !device_ok(dev)) {
-            fprintf(stderr, "liblzf_hip: no gfx950 device %d (devices: %d); the codec runs on the GPU only\n", dev,
-                    n);
-            return;
-        }
-        int prev = -1;
-        (void)hipGetDevice(&prev);
-        (void)hipSetDevice(dev);
-        ok = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess;
-        if (prev >= 0) (void)hipSetDevice(prev);
-    }
-    /* the buffers of this thread (at its exit, or lzf_gpu_release) */
-    void release()
-    {
-        if (!ok) return;
-        int prev = -1;
-        (void)hipGetDevice(&prev);
-        (void)hipSetDevice(dev);
-        if (stream) (void)hipStreamSynchronize(stream);
-        for (auto &sl : slot) {
-            if (sl.stream) (void)hipStreamSynchronize(sl.stream);
-            for (Buf *b : {&sl.d_in, &sl.d_out, &sl.d_meta, &sl.h_in, &sl.h_out, &sl.h_meta}) b->release();
-            sl.busy = false;
-        }
-        for (Buf *b : {&d_in, &d_out, &d_meta, &h_in, &h_out, &h_meta}) b->release();
-        if (prev >= 0) (void)hipSetDevice(prev);
-    }
-    ~Ctx() { release(); }
-};
-
-Ctx &ctx()
-{
-    static thread_local Ctx c;
-    if (!c.ok) throw LzfFail{LZF_GPU_ENODEV};
-    return c;
-}
-
-/* Run f(lo, hi) over [0, n) split into up to `threads` ranges. */
-template <class F> void parallel_ranges(uint32_t n, uint32_t threads, F f)
-{
-    if (threads <= 1 || n < 2u * threads) {
-        f(0u, n);
-        return;
-    }
-    std::vector<std::thread> ts;
-    const uint32_t per = (n + threads - 1u) / threads;
-    for (uint32_t t = 1; t < threads; t++) {
-        const uint32_t lo = t * per, hi = lo + per < n ? lo + per : n;
-        if (lo < hi) ts.emplace_back([=]() { f(lo, hi); });
-    }
-    f(0u, per < n ? per : n);
-    for (auto &t : ts) t.join();
-}
-
-uint32_t host_threads()
-{
-    const char *e = getenv("LZF_GPU_HOST_THREADS");
-    if (e) return (uint32_t)atoi(e) > 0 ? (uint32_t)atoi(e) : 1u;
-    const unsigned hc = std::thread::hardware_concurrency();
-    return hc >= 8u ? 8u : (hc ? hc : 1u);
-}
-
-/* Large host batches: values in chunks through two slots on two streams.
- * The CPU gathers chunk k+1's values (several threads) while chunk k moves
- * over PCIe and runs; results are scattered back once a slot comes round
- * again.  Each chunk's values are packed (inputs back to back, outputs at
- * their caps back to back), so only their bytes cross the bus. */
-int host_batch_pipelined(bool compress, const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
-                         uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len,
-                         int32_t *err, uint32_t count, uint64_t chunk_in, uint64_t chunk_out)
-{
-    Ctx &c = ctx();
-    DeviceGuard g(c.dev);
-    const uint32_t threads = host_threads();
-    for (auto &sl : c.slot) {
-        if (!sl.stream) check(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking), "hipStreamCreate");
-        if (!sl.done) check(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming), "hipEventCreate");
-        sl.busy = false;
-    }
-    const size_t mrec = 2 * sizeof(uint64_t) + 3 * sizeof(uint32_t) + sizeof(int32_t);
-    /* results of a finished slot back to the caller's arrays */
-    auto drain = [&](Slot &sl) {
-        if (!sl.busy) return;
-        check(hipEventSynchronize(sl.done), "hipEventSynchronize");
-        const uint32_t n = sl.count;
-        const uint64_t *m_out_off = (const uint64_t *)sl.h_meta.p + n;
-        const uint32_t *m_out_len = (const uint32_t *)(m_out_off + n) + 2u * n;
-        const int32_t *m_err = (const int32_t *)(m_out_len + n);
-        const uint8_t *h_out = (const uint8_t *)sl.h_out.p;
-        parallel_ranges(n, threads, [&](uint32_t lo, uint32_t hi) {
-            for (uint32_t k = lo; k < hi; k++) {
-                const uint32_t i = sl.first + k;
-                out_len[i] = m_out_len[k];
-                if (err) err[i] = m_err[k];
-                if (m_out_len[k]) memcpy(out + out_off[i], h_out + m_out_off[k], m_out_len[k]);
-            }
-        });
-        sl.busy = false;
-    };
-    uint32_t i0 = 0, k = 0;
-    while (i0 < count) {
-        /* the chunk: values [i0, i1) */
-        uint64_t bin = 0, bout = 0;
-        uint32_t i1 = i0, max_len = 0;
-        while (i1 < count) {
-            const uint64_t li = in_len[i1] ? in_len[i1] : 1u;     /* a 0-length stream reads 1 byte */
-            if (i1 > i0 && (bin + li > chunk_in || bout + out_cap[i1] > chunk_out)) break;
-            bin += li;
-            bout += out_cap[i1];
-            const uint32_t l = compress ? in_len[i1] : out_cap[i1];
-            if (l > max_len) max_len = l;
-            i1++;
-        }
-        Slot &sl = c.slot[k & 1u];
-        drain(sl);
-        const uint32_t n = i1 - i0;
-        uint8_t *h_in = (uint8_t *)sl.h_in.get(bin);
-        uint8_t *h_meta = (uint8_t *)sl.h_meta.get((size_t)n * mrec);
-        uint8_t *d_in = (uint8_t *)sl.d_in.get(bin);
-        uint8_t *d_out = (uint8_t *)sl.d_out.get(bout);
-        uint8_t *d_meta = (uint8_t *)sl.d_meta.get((size_t)n * mrec);
-        sl.h_out.get(bout);
-        uint64_t *m_in_off = (uint64_t *)h_meta, *m_out_off = m_in_off + n;
-        uint32_t *m_in_len = (uint32_t *)(m_out_off + n), *m_out_cap = m_in_len + n;
-        {
-            uint64_t a = 0, b = 0;
-            for (uint32_t j = 0; j < n; j++) {
-                const uint32_t i = i0 + j;
-                m_in_off[j] = a;
-                m_out_off[j] = b;
-                m_in_len[j] = in_len[i];
-                m_out_cap[j] = out_cap[i];
-                a += in_len[i] ? in_len[i] : 1u;
-                b += out_cap[i];
-            }
-        }
-        parallel_ranges(n, threads, [&](uint32_t lo, uint32_t hi) {
-            for (uint32_t j = lo; j < hi; j++) {
-                const uint32_t i = i0 + j;
-                memcpy(h_in + m_in_off[j], in + in_off[i], in_len[i] ? in_len[i] : 1u);
-            }
-        });
-        const size_t res_off = (uint8_t *)(m_out_cap + n) - h_meta;
-        check(hipMemcpyAsync(d_in, h_in, bin, hipMemcpyHostToDevice, sl.stream), "hipMemcpyAsync");
-        check(hipMemcpyAsync(d_meta, h_meta, res_off, hipMemcpyHostToDevice, sl.stream), "hipMemcpyAsync");
-        LzfBatch b{};
-        b.in = d_in;
-        b.in_off = (const uint64_t *)d_meta;
-        b.out_off = b.in_off + n;
-        b.in_len = (const uint32_t *)(b.out_off + n);
-        b.out_cap = b.in_len + n;
-        b.out_len = (uint32_t *)(b.out_cap + n);
-        b.err = (int32_t *)(b.out_len + n);
-        b.out = d_out;
-        b.count = n;
-        b.max_len = max_len;
-        check(compress ? launch_compress(b, sl.stream) : launch_decompress(b, sl.stream), "kernel launch");
-        check(hipMemcpyAsync(h_meta + res_off, d_meta + res_off, (size_t)n * mrec - res_off,
-                             hipMemcpyDeviceToHost, sl.stream), "hipMemcpyAsync");
-        check(hipMemcpyAsync(sl.h_out.p, d_out, bout, hipMemcpyDeviceToHost, sl.stream), "hipMemcpyAsync");
-        check(hipEventRecord(sl.done, sl.stream), "hipEventRecord");
-        sl.first = i0;
-        sl.count = n;
-        sl.busy = true;
-        i0 = i1;
-        k++;
-    }
-    drain(c.slot[k & 1u]);
-    drain(c.slot[(k + 1u) & 1u]);
-    return LZF_GPU_OK;
-}
-
-/* Host batch: stage arena + descriptors, run, copy back. */
-int host_batch(bool compress, const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
-               uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len,
-               int32_t *err, uint32_t count)
-{
-    if (!count || !in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len)
-        return LZF_GPU_EARG;
-    {
-        /* large batches whose outputs are not much bigger than their inputs
-         * (compress, or decompress with caps near the values' sizes) go
-         * through the chunked pipeline */
-        uint64_t sin = 0, sout = 0;
-        for (uint32_t i = 0; i < count; i++) {
-            sin += in_len[i] ? in_len[i] : 1u;
-            sout += out_cap[i];
-        }
-        const uint64_t chunk = 32ull << 20;
-        if (sin >= 2 * chunk && sout <= 4 * sin)
-            return host_batch_pipelined(compress, in, in_off, in_len, out, out_off, out_cap, out_len, err,
-                                        count, chunk, 4 * chunk);
-    }
-    Ctx &c = ctx();
-    DeviceGuard g(c.dev);
-    uint64_t in_end = 0, out_end = 0;
-    uint32_t max_len = 0;
-    for (uint32_t i = 0; i < count; i++) {
-        uint64_t ie = in_off[i] + (in_len[i] ? in_len[i] : 1u);   /* a 0-length stream reads 1 byte */
-        uint64_t oe = out_off[i] + out_cap[i];
-        if (ie > in_end) in_end = ie;
-        if (oe > out_end) out_end = oe;
-        uint32_t l = compress ? in_len[i] : out_cap[i];
-        if (l > max_len) max_len = l;
-    }
-    size_t meta_bytes = (size_t)count * (2 * sizeof(uint64_t) + 3 * sizeof(uint32_t) + sizeof(int32_t));
-    uint8_t *h_in = (uint8_t *)c.h_in.get(in_end);
-    uint8_t *h_meta = (uint8_t *)c.h_meta.get(meta_bytes);
-    uint8_t *d_in = (uint8_t *)c.d_in.get(in_end);
-    uint8_t *d_out = (uint8_t *)c.d_out.get(out_end);
-    uint8_t *d_meta = (uint8_t *)c.d_meta.get(meta_bytes);
-    memcpy(h_in, in, in_end);
-    uint64_t *m_in_off = (uint64_t *)h_meta;
-    uint64_t *m_out_off = m_in_off + count;
-    uint32_t *m_in_len = (uint32_t *)(m_out_off + count);
-    uint32_t *m_out_cap = m_in_len + count;
-    uint32_t *m_out_len = m_out_cap + count;
-    int32_t *m_err = (int32_t *)(m_out_len + count);
-    memcpy(m_in_off, in_off, count * sizeof(uint64_t));
-    memcpy(m_out_off, out_off, count * sizeof(uint64_t));
-    memcpy(m_in_len, in_len, count * sizeof(uint32_t));
-    memcpy(m_out_cap, out_cap, count * sizeof(uint32_t));
-    size_t res_off = (uint8_t *)m_out_len - h_meta;
-    check(hipMemcpyAsync(d_in, h_in, in_end, hipMemcpyHostToDevice, c.stream), "hipMemcpyAsync");
-    check(hipMemcpyAsync(d_meta, h_meta, res_off, hipMemcpyHostToDevice, c.stream), "hipMemcpyAsync");
-    LzfBatch b{};
-    b.in = d_in;
-    b.in_off = (const uint64_t *)d_meta;
-    b.out_off = b.in_off + count;
-    b.in_len = (const uint32_t *)(b.out_off + count);
-    b.out_cap = b.in_len + count;
-    b.out_len = (uint32_t *)(b.out_cap + count);
-    b.err = (int32_t *)(b.out_len + count);
-    b.out = d_out;
-    b.count = count;
-    b.max_len = max_len;
-    check(compress ? launch_compress(b, c.stream) : launch_decompress(b, c.stream), "kernel launch");
-    check(hipMemcpyAsync(h_meta + res_off, d_meta + res_off, meta_bytes - res_off,
-                         hipMemcpyDeviceToHost, c.stream), "hipMemcpyAsync");
-    check(hipStreamSynchronize(c.stream), "hipStreamSynchronize");
-    memcpy(out_len, m_out_len, count * sizeof(uint32_t));
-    if (err) memcpy(err, m_err, count * sizeof(int32_t));
-    /* copy back only the produced bytes of each value */
-    uint64_t lo = ~0ull, hi = 0;
-    for (uint32_t i = 0; i < count; i++) {
-        if (!m_out_len[i]) continue;
-        if (out_off[i] < lo) lo = out_off[i];
-        if (out_off[i] + m_out_len[i] > hi) hi = out_off[i] + m_out_len[i];
-    }
-    if (hi > lo) {
-        uint8_t *h_out = (uint8_t *)c.h_out.get(hi - lo);
-        check(hipMemcpyAsync(h_out, d_out + lo, hi - lo, hipMemcpyDeviceToHost, c.stream),
-              "hipMemcpyAsync");
-        check(hipStreamSynchronize(c.stream), "hipStreamSynchronize");
-        for (uint32_t i = 0; i < count; i++)
-            if (m_out_len[i]) memcpy(out + out_off[i], h_out + (out_off[i] - lo), m_out_len[i]);
-    }
-    return LZF_GPU_OK;
-}
-
-/* host_batch with the failure of a library call as a return code; the
- * streams of the thread's context are drained so its buffers are free */
-int host_batch_rc(bool compress, const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
-                  uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len,
-                  int32_t *err, uint32_t count)
-{
-    try {
-        return host_batch(compress, in, in_off, in_len, out, out_off, out_cap, out_len, err, count);
-    } catch (const LzfFail &f) {
-        try {
-            Ctx &c = ctx();
-            if (c.stream) (void)hipStreamSynchronize(c.stream);
-            for (auto &sl : c.slot) {
-                if (sl.stream) (void)hipStreamSynchronize(sl.stream);
-                sl.busy = false;
-            }
-            (void)hipGetLastError();
-        } catch (const LzfFail &) {
-        }
-        return f.code;
-    }
-}
-
-/* decoded sizes of host streams (the pre-pass of lzf_dsize.hip) */
-int host_dsize(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, uint32_t *out_size,
-               int32_t *err, uint32_t count, uint32_t limit)
-{
-    if (!count || !in || !in_off || !in_len || !out_size || !err) return LZF_GPU_EARG;
-    try {
-        Ctx &c = ctx();
-        DeviceGuard g(c.dev);
-        uint64_t in_end = 0;
-        for (uint32_t i = 0; i < count; i++) {
-            const uint64_t ie = in_off[i] + (in_len[i] ? in_len[i] : 1u);   /* a 0-length stream reads 1 byte */
-            if (ie > in_end) in_end = ie;
-        }
-        const size_t mb = (size_t)count * (sizeof(uint64_t) + 3 * sizeof(uint32_t));
-        uint8_t *h_in = (uint8_t *)c.h_in.get(in_end), *h_meta = (uint8_t *)c.h_meta.get(mb);
-        uint8_t *d_in = (uint8_t *)c.d_in.get(in_end), *d_meta = (uint8_t *)c.d_meta.get(mb);
-        memcpy(h_in, in, in_end);
-        memcpy(h_meta, in_off, count * sizeof(uint64_t));
-        memcpy(h_meta + count * sizeof(uint64_t), in_len, count * sizeof(uint32_t));
-        const size_t res = count * (sizeof(uint64_t) + sizeof(uint32_t));
-        check(hipMemcpyAsync(d_in, h_in, in_end, hipMemcpyHostToDevice, c.stream), "hipMemcpyAsync");
-        check(hipMemcpyAsync(d_meta, h_meta, res, hipMemcpyHostToDevice, c.stream), "hipMemcpyAsync");
-        check(lzf_launch_dsize(d_in, (const uint64_t *)d_meta, (const uint32_t *)(d_meta + count * sizeof(uint64_t)),
-                               (uint32_t *)(d_meta + res), (int32_t *)(d_meta + res + count * sizeof(uint32_t)), count,
-                               limit, c.stream),
-              "kernel launch");
-        check(hipMemcpyAsync(h_meta + res, d_meta + res, mb - res, hipMemcpyDeviceToHost, c.stream),
-              "hipMemcpyAsync");
-        check(hipStreamSynchronize(c.stream), "hipStreamSynchronize");
-        memcpy(out_size, h_meta + res, count * sizeof(uint32_t));
-        memcpy(err, h_meta + res + count * sizeof(uint32_t), count * sizeof(int32_t));
-        return LZF_GPU_OK;
-    } catch (const LzfFail &f) {
-        return f.code;
-    }
-}
-
 }  // namespace
 
+/* the routed launches and the scratch, for the host-memory paths (lzf_host.cpp) */
+hipError_t lzf_route_compress(const LzfBatch &b, hipStream_t s) { return launch_compress(b, s); }
+hipError_t lzf_route_decompress(const LzfBatch &b, hipStream_t s) { return launch_decompress(b, s); }
+uint32_t lzf_route_min_count(uint32_t max_len) { return lane_min_count(max_len); }
+bool lzf_device_ok(int dev) { return device_ok(dev); }
+void lzf_scratch_release_all(void)
+{
+    for (Scratch &S : g_scratch) {
+        std::lock_guard<std::mutex> lk(S.mu);
+        scratch_free(S);
+    }
+}
+
 extern "C" {
-
-/* Single calls are batches of one.  A failure of the device path (no usable
- * gfx950, a HIP error) is reported, never aborted on: lzf_compress returns 0,
- * which the caller already reads as "store the value plain"
- * (src/query.c:393-397); lzf_decompress returns 0 with errno EIO, an errno the
- * reference codec never sets (src/lzf.h:85-91 lists E2BIG and EINVAL). */
-unsigned int lzf_compress(const void *const in_data, unsigned int in_len, void *out_data,
-                          unsigned int out_len)
-{
-    if (!in_len || !out_len) return 0;                    /* src/lzf_c.c:131 */
-    if (!in_data || !out_data) return 0;
-    uint64_t zero = 0;
-    uint32_t res = 0;
-    const int rc = host_batch_rc(true, (const uint8_t *)in_data, &zero, &in_len, (uint8_t *)out_data, &zero,
-                                 &out_len, &res, nullptr, 1);
-    return rc == LZF_GPU_OK ? res : 0u;
-}
-
-unsigned int lzf_decompress(const void *const in_data, unsigned int in_len, void *out_data,
-                            unsigned int out_len)
-{
-    uint8_t none = 0;
-    if (!in_data || (!out_data && out_len)) {             /* the reference would fault */
-        errno = EINVAL;
-        return 0;
-    }
-    if (!out_data) out_data = &none;                      /* out_len 0: nothing is written */
-    uint64_t zero = 0;
-    uint32_t res = 0;
-    int32_t err = 0;
-    const int rc = host_batch_rc(false, (const uint8_t *)in_data, &zero, &in_len, (uint8_t *)out_data, &zero,
-                                 &out_len, &res, &err, 1);
-    if (rc != LZF_GPU_OK) {
-        errno = EIO;
-        return 0;
-    }
-    if (!res) errno = err ? err : EINVAL;
-    return res;
-}
 
 int lzf_gpu_compress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
                            uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
@@ -830,18 +387,6 @@ int lzf_gpu_decompress_batch(const uint8_t *in, const uint64_t *in_off, const ui
     return e == hipSuccess ? LZF_GPU_OK : code_of(e);
 }
 
-void lzf_gpu_release(void)
-{
-    for (Scratch &S : g_scratch) {
-        std::lock_guard<std::mutex> lk(S.mu);
-        scratch_free(S);
-    }
-    try {
-        ctx().release();
-    } catch (const LzfFail &) {
-    }
-}
-
 int lzf_gpu_synth_fill(int kind, uint64_t seed, uint64_t first, uint64_t stride, uint32_t count,
                        uint32_t n, uint8_t *out, void *stream)
 {
@@ -854,20 +399,6 @@ int lzf_gpu_synth_fill(int kind, uint64_t seed, uint64_t first, uint64_t stride,
                : LZF_GPU_ELAUNCH;
 }
 
-int lzf_host_compress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
-                            uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
-                            uint32_t *out_len, uint32_t count)
-{
-    return host_batch_rc(true, in, in_off, in_len, out, out_off, out_cap, out_len, nullptr, count);
-}
-
-int lzf_host_decompress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
-                              uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
-                              uint32_t *out_len, int32_t *err, uint32_t count)
-{
-    return host_batch_rc(false, in, in_off, in_len, out, out_off, out_cap, out_len, err, count);
-}
-
 int lzf_gpu_decoded_size_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
                                uint32_t *out_size, int32_t *err, uint32_t count, uint32_t out_limit, void *stream)
 {
@@ -877,12 +408,6 @@ int lzf_gpu_decoded_size_batch(const uint8_t *in, const uint64_t *in_off, const 
     return lzf_launch_dsize(in, in_off, in_len, out_size, err, count, out_limit, (hipStream_t)stream) == hipSuccess
                ? LZF_GPU_OK
                : LZF_GPU_ELAUNCH;
-}
-
-int lzf_host_decoded_size_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
-                                uint32_t *out_size, int32_t *err, uint32_t count, uint32_t out_limit)
-{
-    return host_dsize(in, in_off, in_len, out_size, err, count, out_limit);
 }
 
 uint64_t lzf_gpu_kv_frame_work_size(uint32_t count)

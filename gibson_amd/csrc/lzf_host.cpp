@@ -1,0 +1,1143 @@
+/*
+ * lzf_host.cpp -- the host-memory side of liblzf_hip.so.
+ *
+ * The drop-in pair of include/lzf.h (src/lzf.h:76-78, 95-97, replacing
+ * src/lzf_c.c:98 and src/lzf_d.c:55) and the host-memory batch calls of
+ * include/lzf_gpu.h.  Gibson's path starts in host memory -- the client's
+ * request buffer (src/server.c:180) on the way in, the trie-resident value
+ * (src/query.c:409) on the way out -- so these calls move values over PCIe,
+ * run the routed kernels (lzf_api.cpp) and bring the results back.
+ *
+ * Devices.  Gibson is one process with one event loop
+ * (src/net.c:578-589, README.md:13); the only place it can use several GPUs
+ * is this library.  LZF_GPU_DEVICES names them ("0,1,2,3", "all"; a device
+ * may repeat: "0,0" runs two contexts on device 0).  A host batch sends value
+ * i to entry i mod G; each entry has a persistent worker thread with its own
+ * non-blocking streams, pinned staging and, on its device, the shared compress
+ * scratch.  The worker binds itself to its device's NUMA node (read from
+ * sysfs through the PCI bus id) before it allocates anything, so its pinned
+ * staging is node-local.  Results land at index i; a failing entry makes the
+ * batch return its LZF_GPU_E* code, never an abort.  Unset, LZF_GPU_DEVICE
+ * (default 0) is the one device and batches run on the calling thread.
+ *
+ * Moving bytes.  Two paths, same results:
+ *  - registered (lzf_host_register): the caller's arenas are page-locked and
+ *    mapped, so the GPU reads each value from, and writes each stream to,
+ *    the caller's memory itself (lzf_hostio.hip) -- or the DMA engines copy
+ *    runs of adjacent values -- and the CPU touches only descriptors;
+ *  - staged (anything else): the CPU packs values into pinned staging and
+ *    unpacks the results (several threads), in a two-slot chunk pipeline for
+ *    large batches.
+ */
+#include <ctype.h>
+#include <errno.h>
+#include <pthread.h>
+#include <sched.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <iterator>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "lzf_internal.h"
+#include "../../include/lzf.h"
+#include "../../include/lzf_gpu.h"
+
+namespace {
+
+/* Library failures inside the host-memory paths are thrown as LzfFail and
+ * turned into an LZF_GPU_E* code at the C boundary (never abort: a transient
+ * HIP error must not take the server down). */
+struct LzfFail {
+    int code;
+};
+
+int code_of(hipError_t e)
+{
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return LZF_GPU_ENOMEM;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return LZF_GPU_ENODEV;
+    return LZF_GPU_ELAUNCH;
+}
+
+void check(hipError_t e, const char *what)
+{
+    if (e == hipSuccess) return;
+    static bool said = false;
+    if (!said) {
+        said = true;
+        fprintf(stderr, "liblzf_hip: %s failed: %s\n", what, hipGetErrorString(e));
+    }
+    (void)hipGetLastError();
+    throw LzfFail{code_of(e)};
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) check(hipSetDevice(dev), "hipSetDevice");
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+/* ---- the device plan (LZF_GPU_DEVICES) ---------------------------------- */
+
+struct Plan {
+    std::vector<int> dev;
+    int rc = LZF_GPU_OK;
+};
+
+const Plan &plan()
+{
+    static const Plan p = [] {
+        Plan q;
+        const char *e = getenv("LZF_GPU_DEVICES");
+        if (!e || !*e) {
+            const char *d = getenv("LZF_GPU_DEVICE");
+            q.dev.push_back(d ? atoi(d) : 0);
+            return q;
+        }
+        int visible = 0;
+        if (hipGetDeviceCount(&visible) != hipSuccess) visible = 0;
+        int buf[64];
+        const int n = lzf_gpu_parse_device_list(e, visible, buf, 64);
+        if (n <= 0) {
+            fprintf(stderr, "liblzf_hip: LZF_GPU_DEVICES=\"%s\" names no usable device (%d visible)\n", e, visible);
+            q.rc = LZF_GPU_ENODEV;
+            q.dev.push_back(0);
+            return q;
+        }
+        for (int k = 0; k < n; k++) {
+            if (!lzf_device_ok(buf[k])) {
+                fprintf(stderr, "liblzf_hip: LZF_GPU_DEVICES entry %d (device %d) is not a gfx950\n", k, buf[k]);
+                q.rc = LZF_GPU_ENODEV;
+            }
+            q.dev.push_back(buf[k]);
+        }
+        return q;
+    }();
+    return p;
+}
+
+/* ---- NUMA: the node of a device and binding a thread to it --------------- */
+
+bool parse_cpulist(const char *s, cpu_set_t *set)
+{
+    CPU_ZERO(set);
+    bool any = false;
+    while (*s) {
+        char *end;
+        long a = strtol(s, &end, 10);
+        if (end == s) break;
+        long b = a;
+        s = end;
+        if (*s == '-') {
+            b = strtol(s + 1, &end, 10);
+            s = end;
+        }
+        for (long c = a; c <= b && c < CPU_SETSIZE; c++) {
+            CPU_SET((int)c, set);
+            any = true;
+        }
+        if (*s == ',') s++;
+        else break;
+    }
+    return any;
+}
+
+/* the device's NUMA node from sysfs (-1: unknown) and that node's CPUs */
+int device_numa(int dev, cpu_set_t *cpus)
+{
+    CPU_ZERO(cpus);
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, dev) != hipSuccess) return -1;
+    for (char *c = bus; *c; c++) *c = (char)tolower((unsigned char)*c);
+    const std::string base = std::string("/sys/bus/pci/devices/") + bus;
+    int node = -1;
+    if (FILE *f = fopen((base + "/numa_node").c_str(), "r")) {
+        if (fscanf(f, "%d", &node) != 1) node = -1;
+        fclose(f);
+    }
+    if (FILE *f = fopen((base + "/local_cpulist").c_str(), "r")) {
+        char line[4096] = {0};
+        if (fgets(line, sizeof line, f)) parse_cpulist(line, cpus);
+        fclose(f);
+    }
+    return node;
+}
+
+/* Pin the calling thread to the node's CPUs that this process may use and
+ * prefer the node for its memory (set_mempolicy MPOL_PREFERRED; pinned
+ * staging is then allocated with hipHostMallocNumaUser).  False when the
+ * node is unknown or none of its CPUs is in the process's affinity set. */
+bool bind_to_node(int node, const cpu_set_t &local)
+{
+    if (node < 0 || node >= 1024) return false;
+    cpu_set_t allowed, both;
+    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return false;
+    CPU_AND(&both, &allowed, &local);
+    if (CPU_COUNT(&both) == 0) return false;
+    if (pthread_setaffinity_np(pthread_self(), sizeof both, &both) != 0) return false;
+    unsigned long mask[1024 / (8 * sizeof(unsigned long))] = {0};
+    mask[node / (8 * sizeof(unsigned long))] |= 1ul << (node % (8 * sizeof(unsigned long)));
+    const long MPOL_PREFERRED_ = 1;
+    return syscall(SYS_set_mempolicy, MPOL_PREFERRED_, mask, (unsigned long)1024) == 0;
+}
+
+/* ---- per-thread contexts ------------------------------------------------- */
+
+/* Growable device / pinned buffers of one context. */
+struct Buf {
+    void *p = nullptr;
+    size_t cap = 0;
+    bool pinned = false;
+    unsigned flags = hipHostMallocDefault;
+    void *get(size_t need)
+    {
+        if (need == 0) need = 1;
+        if (need <= cap) return p;
+        size_t want = need + need / 4 + 256;
+        if (p) { pinned ? (void)hipHostFree(p) : (void)hipFree(p); }
+        p = nullptr;
+        cap = 0;
+        hipError_t e = pinned ? hipHostMalloc(&p, want, flags) : hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            p = nullptr;
+            check(e, pinned ? "hipHostMalloc" : "hipMalloc");
+        }
+        cap = want;
+        return p;
+    }
+    void release()
+    {
+        if (p) { pinned ? (void)hipHostFree(p) : (void)hipFree(p); }
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+/* One stage of a chunk pipeline: its own stream, pinned and device buffers,
+ * and the chunk it holds until its results are taken. */
+struct Slot {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    Buf d_in, d_out, d_meta;
+    Buf h_in{nullptr, 0, true}, h_out{nullptr, 0, true}, h_meta{nullptr, 0, true};
+    uint32_t first = 0, count = 0;
+    bool busy = false;
+};
+
+struct Ctx {
+    int dev = 0;
+    bool ok = false;
+    bool numa_bound = false;
+    hipStream_t stream = nullptr;
+    Buf d_in, d_out, d_meta;
+    Buf h_in{nullptr, 0, true}, h_out{nullptr, 0, true}, h_meta{nullptr, 0, true};
+    Slot slot[2];
+    Ctx(int device, bool bound) : dev(device), numa_bound(bound)
+    {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || dev < 0 || dev >= n || !lzf_device_ok(dev)) {
+            fprintf(stderr, "liblzf_hip: no gfx950 device %d (devices: %d); the codec runs on the GPU only\n", dev,
+                    n);
+            return;
+        }
+        const unsigned fl = bound ? (unsigned)hipHostMallocNumaUser : (unsigned)hipHostMallocDefault;
+        for (Buf *b : {&h_in, &h_out, &h_meta}) b->flags = fl;
+        for (auto &sl : slot)
+            for (Buf *b : {&sl.h_in, &sl.h_out, &sl.h_meta}) b->flags = fl;
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(dev);
+        ok = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess;
+        if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+    }
+    /* this context's buffers (at its thread's exit, or lzf_gpu_release) */
+    void release()
+    {
+        if (!ok) return;
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(dev);
+        if (stream) (void)hipStreamSynchronize(stream);
+        for (auto &sl : slot) {
+            if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+            for (Buf *b : {&sl.d_in, &sl.d_out, &sl.d_meta, &sl.h_in, &sl.h_out, &sl.h_meta}) b->release();
+            sl.busy = false;
+        }
+        for (Buf *b : {&d_in, &d_out, &d_meta, &h_in, &h_out, &h_meta}) b->release();
+        if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+    }
+    /* after a failure: wait for what is in flight, so the buffers are free */
+    void quiesce()
+    {
+        if (!ok) return;
+        if (stream) (void)hipStreamSynchronize(stream);
+        for (auto &sl : slot) {
+            if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+            sl.busy = false;
+        }
+        (void)hipGetLastError();
+    }
+    ~Ctx() { release(); }
+};
+
+/* the calling thread's context, on the plan's first device */
+Ctx &caller_ctx()
+{
+    static thread_local Ctx c(plan().dev[0], false);
+    if (!c.ok) throw LzfFail{LZF_GPU_ENODEV};
+    return c;
+}
+
+/* ---- registered host ranges (lzf_host_register) --------------------------- */
+
+std::mutex g_reg_mu;
+std::map<uintptr_t, uintptr_t> g_reg;      /* start -> end of each registered range */
+
+/* true when [lo, hi) lies inside one registered range */
+bool is_registered(uintptr_t lo, uintptr_t hi)
+{
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg.upper_bound(lo);
+    if (it == g_reg.begin()) return false;
+    --it;
+    return lo >= it->first && hi <= it->second;
+}
+
+/* ---- one host batch ------------------------------------------------------ */
+
+/* the caller's arrays of one host-memory call */
+struct HostArgs {
+    bool compress;
+    const uint8_t *in;
+    const uint64_t *in_off;
+    const uint32_t *in_len;
+    uint8_t *out;
+    const uint64_t *out_off;
+    const uint32_t *out_cap;
+    uint32_t *out_len;
+    int32_t *err;
+};
+
+/* value k of a sub-batch is the caller's value first + k * stride */
+struct View {
+    uint32_t first = 0, stride = 1, count = 0;
+    uint32_t at(uint32_t k) const { return first + k * stride; }
+};
+
+/* a 0-length stream still reads its first control byte (src/lzf_d.c:64-66) */
+inline uint32_t in_extent(const HostArgs &a, uint32_t i)
+{
+    return a.in_len[i] ? a.in_len[i] : (a.compress ? 0u : 1u);
+}
+
+/* Run f(lo, hi) over [0, n) split into up to `threads` ranges. */
+template <class F> void parallel_ranges(uint32_t n, uint32_t threads, F f)
+{
+    if (threads <= 1 || n < 2u * threads) {
+        f(0u, n);
+        return;
+    }
+    std::vector<std::thread> ts;
+    const uint32_t per = (n + threads - 1u) / threads;
+    for (uint32_t t = 1; t < threads; t++) {
+        const uint32_t lo = t * per, hi = lo + per < n ? lo + per : n;
+        if (lo < hi) ts.emplace_back([=]() { f(lo, hi); });
+    }
+    f(0u, per < n ? per : n);
+    for (auto &t : ts) t.join();
+}
+
+uint32_t host_threads()
+{
+    const char *e = getenv("LZF_GPU_HOST_THREADS");
+    if (e) return (uint32_t)atoi(e) > 0 ? (uint32_t)atoi(e) : 1u;
+    const unsigned hc = std::thread::hardware_concurrency();
+    return hc >= 8u ? 8u : (hc ? hc : 1u);
+}
+
+hipError_t launch(const HostArgs &a, const LzfBatch &b, hipStream_t s)
+{
+    return a.compress ? lzf_route_compress(b, s) : lzf_route_decompress(b, s);
+}
+
+void make_slot_streams(Ctx &c)
+{
+    for (auto &sl : c.slot) {
+        if (!sl.stream) check(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking), "hipStreamCreate");
+        if (!sl.done) check(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming), "hipEventCreate");
+        sl.busy = false;
+    }
+}
+
+/* Staged, chunked: values in chunks through two slots on two streams.  The
+ * CPU packs chunk k+1's values into pinned staging (several threads) while
+ * chunk k moves over PCIe and runs; results are unpacked once a slot comes
+ * round again.  Each chunk's values are packed (inputs back to back, outputs
+ * at their caps back to back), so only their bytes cross the bus. */
+void host_batch_staged(Ctx &c, const HostArgs &a, const View &v, uint64_t chunk_in, uint64_t chunk_out)
+{
+    const uint32_t threads = host_threads();
+    make_slot_streams(c);
+    const size_t mrec = 2 * sizeof(uint64_t) + 4 * sizeof(uint32_t);
+    auto drain = [&](Slot &sl) {
+        if (!sl.busy) return;
+        check(hipEventSynchronize(sl.done), "hipEventSynchronize");
+        const uint32_t n = sl.count;
+        const uint64_t *m_out_off = (const uint64_t *)sl.h_meta.p + n;
+        const uint32_t *m_out_len = (const uint32_t *)(m_out_off + n) + 2u * n;
+        const int32_t *m_err = (const int32_t *)(m_out_len + n);
+        const uint8_t *h_out = (const uint8_t *)sl.h_out.p;
+        parallel_ranges(n, threads, [&](uint32_t lo, uint32_t hi) {
+            for (uint32_t k = lo; k < hi; k++) {
+                const uint32_t i = v.at(sl.first + k);
+                a.out_len[i] = m_out_len[k];
+                if (a.err) a.err[i] = m_err[k];
+                if (m_out_len[k]) memcpy(a.out + a.out_off[i], h_out + m_out_off[k], m_out_len[k]);
+            }
+        });
+        sl.busy = false;
+    };
+    uint32_t k0 = 0, round = 0;
+    while (k0 < v.count) {
+        uint64_t bin = 0, bout = 0;
+        uint32_t k1 = k0, max_len = 0;
+        while (k1 < v.count) {
+            const uint32_t i = v.at(k1);
+            const uint64_t li = in_extent(a, i) ? in_extent(a, i) : 1u;
+            if (k1 > k0 && (bin + li > chunk_in || bout + a.out_cap[i] > chunk_out)) break;
+            bin += li;
+            bout += a.out_cap[i];
+            const uint32_t l = a.compress ? a.in_len[i] : a.out_cap[i];
+            if (l > max_len) max_len = l;
+            k1++;
+        }
+        Slot &sl = c.slot[round & 1u];
+        drain(sl);
+        const uint32_t n = k1 - k0;
+        uint8_t *h_in = (uint8_t *)sl.h_in.get(bin);
+        uint8_t *h_meta = (uint8_t *)sl.h_meta.get((size_t)n * mrec);
+        uint8_t *d_in = (uint8_t *)sl.d_in.get(bin);
+        uint8_t *d_out = (uint8_t *)sl.d_out.get(bout);
+        uint8_t *d_meta = (uint8_t *)sl.d_meta.get((size_t)n * mrec);
+        sl.h_out.get(bout);
+        uint64_t *m_in_off = (uint64_t *)h_meta, *m_out_off = m_in_off + n;
+        uint32_t *m_in_len = (uint32_t *)(m_out_off + n), *m_out_cap = m_in_len + n;
+        {
+            uint64_t x = 0, y = 0;
+            for (uint32_t j = 0; j < n; j++) {
+                const uint32_t i = v.at(k0 + j);
+                m_in_off[j] = x;
+                m_out_off[j] = y;
+                m_in_len[j] = a.in_len[i];
+                m_out_cap[j] = a.out_cap[i];
+                x += in_extent(a, i) ? in_extent(a, i) : 1u;
+                y += a.out_cap[i];
+            }
+        }
+        parallel_ranges(n, threads, [&](uint32_t lo, uint32_t hi) {
+            for (uint32_t j = lo; j < hi; j++) {
+                const uint32_t i = v.at(k0 + j);
+                if (in_extent(a, i)) memcpy(h_in + m_in_off[j], a.in + a.in_off[i], in_extent(a, i));
+            }
+        });
+        const size_t res_off = (uint8_t *)(m_out_cap + n) - h_meta;
+        check(hipMemcpyAsync(d_in, h_in, bin, hipMemcpyHostToDevice, sl.stream), "hipMemcpyAsync");
+        check(hipMemcpyAsync(d_meta, h_meta, res_off, hipMemcpyHostToDevice, sl.stream), "hipMemcpyAsync");
+        LzfBatch b{};
+        b.in = d_in;
+        b.in_off = (const uint64_t *)d_meta;
+        b.out_off = b.in_off + n;
+        b.in_len = (const uint32_t *)(b.out_off + n);
+        b.out_cap = b.in_len + n;
+        b.out_len = (uint32_t *)(b.out_cap + n);
+        b.err = (int32_t *)(b.out_len + n);
+        b.out = d_out;
+        b.count = n;
+        b.max_len = max_len;
+        check(launch(a, b, sl.stream), "kernel launch");
+        check(hipMemcpyAsync(h_meta + res_off, d_meta + res_off, (size_t)n * mrec - res_off, hipMemcpyDeviceToHost,
+                             sl.stream),
+              "hipMemcpyAsync");
+        check(hipMemcpyAsync(sl.h_out.p, d_out, bout, hipMemcpyDeviceToHost, sl.stream), "hipMemcpyAsync");
+        check(hipEventRecord(sl.done, sl.stream), "hipEventRecord");
+        sl.first = k0;
+        sl.count = n;
+        sl.busy = true;
+        k0 = k1;
+        round++;
+    }
+    drain(c.slot[round & 1u]);
+    drain(c.slot[(round + 1u) & 1u]);
+}
+
+/* Staged, one piece (small batches, and decodes whose caps are far above
+ * their inputs -- the drop-in lzf_decompress at out_len = maxrequestsize):
+ * after the kernel only the produced bytes come back. */
+void host_batch_small(Ctx &c, const HostArgs &a, const View &v)
+{
+    const uint32_t n = v.count;
+    uint64_t bin = 0, bout = 0;
+    uint32_t max_len = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t i = v.at(k);
+        bin += in_extent(a, i) ? in_extent(a, i) : 1u;
+        bout += a.out_cap[i];
+        const uint32_t l = a.compress ? a.in_len[i] : a.out_cap[i];
+        if (l > max_len) max_len = l;
+    }
+    const size_t meta_bytes = (size_t)n * (2 * sizeof(uint64_t) + 4 * sizeof(uint32_t));
+    uint8_t *h_in = (uint8_t *)c.h_in.get(bin);
+    uint8_t *h_meta = (uint8_t *)c.h_meta.get(meta_bytes);
+    uint8_t *d_in = (uint8_t *)c.d_in.get(bin);
+    uint8_t *d_out = (uint8_t *)c.d_out.get(bout);
+    uint8_t *d_meta = (uint8_t *)c.d_meta.get(meta_bytes);
+    uint64_t *m_in_off = (uint64_t *)h_meta, *m_out_off = m_in_off + n;
+    uint32_t *m_in_len = (uint32_t *)(m_out_off + n), *m_out_cap = m_in_len + n;
+    uint32_t *m_out_len = m_out_cap + n;
+    int32_t *m_err = (int32_t *)(m_out_len + n);
+    {
+        uint64_t x = 0, y = 0;
+        for (uint32_t k = 0; k < n; k++) {
+            const uint32_t i = v.at(k);
+            m_in_off[k] = x;
+            m_out_off[k] = y;
+            m_in_len[k] = a.in_len[i];
+            m_out_cap[k] = a.out_cap[i];
+            if (in_extent(a, i)) memcpy(h_in + x, a.in + a.in_off[i], in_extent(a, i));
+            x += in_extent(a, i) ? in_extent(a, i) : 1u;
+            y += a.out_cap[i];
+        }
+    }
+    const size_t res_off = (uint8_t *)m_out_len - h_meta;
+    check(hipMemcpyAsync(d_in, h_in, bin, hipMemcpyHostToDevice, c.stream), "hipMemcpyAsync");
+    check(hipMemcpyAsync(d_meta, h_meta, res_off, hipMemcpyHostToDevice, c.stream), "hipMemcpyAsync");
+    LzfBatch b{};
+    b.in = d_in;
+    b.in_off = (const uint64_t *)d_meta;
+    b.out_off = b.in_off + n;
+    b.in_len = (const uint32_t *)(b.out_off + n);
+    b.out_cap = b.in_len + n;
+    b.out_len = (uint32_t *)(b.out_cap + n);
+    b.err = (int32_t *)(b.out_len + n);
+    b.out = d_out;
+    b.count = n;
+    b.max_len = max_len;
+    check(launch(a, b, c.stream), "kernel launch");
+    check(hipMemcpyAsync(h_meta + res_off, d_meta + res_off, meta_bytes - res_off, hipMemcpyDeviceToHost,
+                         c.stream),
+          "hipMemcpyAsync");
+    check(hipStreamSynchronize(c.stream), "hipStreamSynchronize");
+    /* only the produced bytes come back: [lo, hi) of the packed outputs */
+    uint64_t lo = ~0ull, hi = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t i = v.at(k);
+        a.out_len[i] = m_out_len[k];
+        if (a.err) a.err[i] = m_err[k];
+        if (!m_out_len[k]) continue;
+        if (m_out_off[k] < lo) lo = m_out_off[k];
+        if (m_out_off[k] + m_out_len[k] > hi) hi = m_out_off[k] + m_out_len[k];
+    }
+    if (hi > lo) {
+        uint8_t *h_out = (uint8_t *)c.h_out.get(hi - lo);
+        check(hipMemcpyAsync(h_out, d_out + lo, hi - lo, hipMemcpyDeviceToHost, c.stream), "hipMemcpyAsync");
+        check(hipStreamSynchronize(c.stream), "hipStreamSynchronize");
+        for (uint32_t k = 0; k < n; k++)
+            if (m_out_len[k]) memcpy(a.out + a.out_off[v.at(k)], h_out + (m_out_off[k] - lo), m_out_len[k]);
+    }
+}
+
+/* Registered arenas: no CPU byte copies.  Per chunk: descriptors up (pinned,
+ * 40 B per value), the values into the packed device arena -- the DMA
+ * engines copy runs of values that lie (nearly) back to back in the caller's
+ * arena, the GPU gathers the rest from the mapped arena -- the routed
+ * kernels, then the GPU writes each result's produced bytes into its slot of
+ * the mapped output arena, and out_len / err come back with the descriptors.
+ * Two slots on two streams, so one chunk's transfers overlap the other's
+ * kernels.  Compress chunks hold at least twice the routing's batch
+ * threshold (the parse's time has a per-launch floor). */
+void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *in_map, uint8_t *out_map)
+{
+    make_slot_streams(c);
+    /* per value: src_off, d_in_off, d_out_off, dst_off (u64), in_len, out_cap, out_len, err (u32) */
+    const size_t mrec = 4 * sizeof(uint64_t) + 4 * sizeof(uint32_t);
+    uint64_t total_in = 0;
+    uint32_t max_len_all = 0;
+    for (uint32_t k = 0; k < v.count; k++) {
+        const uint32_t i = v.at(k);
+        total_in += a.compress ? a.in_len[i] : a.out_cap[i];
+        const uint32_t l = a.compress ? a.in_len[i] : a.out_cap[i];
+        if (l > max_len_all) max_len_all = l;
+    }
+    uint64_t chunk_bytes = 1024ull << 20;
+    if (const char *e = getenv("LZF_GPU_HOST_CHUNK_MB")) chunk_bytes = (uint64_t)strtoull(e, nullptr, 10) << 20;
+    if (chunk_bytes < (1u << 20)) chunk_bytes = 1u << 20;
+    uint32_t nchunks = (uint32_t)((total_in + chunk_bytes - 1) / chunk_bytes);
+    if (a.compress) {
+        const uint32_t least = 2u * lzf_route_min_count(max_len_all);
+        const uint32_t most = least ? v.count / least : v.count;
+        if (nchunks > most) nchunks = most;
+    }
+    if (nchunks < 1) nchunks = 1;
+    const uint32_t per_chunk = (v.count + nchunks - 1) / nchunks;
+    const uint32_t min_len = a.compress ? 0u : 1u;
+
+    auto drain = [&](Slot &sl) {
+        if (!sl.busy) return;
+        check(hipEventSynchronize(sl.done), "hipEventSynchronize");
+        const uint32_t n = sl.count;
+        const uint32_t *m_out_len = (const uint32_t *)((const uint64_t *)sl.h_meta.p + 4u * n) + 2u * n;
+        const int32_t *m_err = (const int32_t *)(m_out_len + n);
+        for (uint32_t k = 0; k < n; k++) {
+            const uint32_t i = v.at(sl.first + k);
+            a.out_len[i] = m_out_len[k];
+            if (a.err) a.err[i] = m_err[k];
+        }
+        sl.busy = false;
+    };
+    uint32_t round = 0;
+    for (uint32_t k0 = 0; k0 < v.count; k0 += per_chunk, round++) {
+        const uint32_t n = v.count - k0 < per_chunk ? v.count - k0 : per_chunk;
+        Slot &sl = c.slot[round & 1u];
+        drain(sl);
+        uint8_t *h_meta = (uint8_t *)sl.h_meta.get((size_t)n * mrec);
+        uint64_t *m_src = (uint64_t *)h_meta, *m_din = m_src + n, *m_dout = m_din + n, *m_dst = m_dout + n;
+        uint32_t *m_in_len = (uint32_t *)(m_dst + n), *m_cap = m_in_len + n;
+        /* device offsets keep each value's host address mod 16 (whole 16-byte
+         * moves); runs: consecutive values no more than 256 bytes apart in
+         * the caller's arena are copied as one DMA piece, gap bytes included
+         * (reads only, inside the registered range) */
+        struct Run {
+            uint64_t src, dst, len;
+        };
+        std::vector<Run> runs;
+        uint64_t x = 0, y = 0;
+        uint32_t max_len = 0;
+        for (uint32_t k = 0; k < n; k++) {
+            const uint32_t i = v.at(k0 + k);
+            const uint64_t so = a.in_off[i], ext = in_extent(a, i);
+            if (!runs.empty() && so >= runs.back().src + runs.back().len && so - (runs.back().src + runs.back().len) <= 256u) {
+                Run &r = runs.back();
+                m_din[k] = r.dst + (so - r.src);
+                r.len = so + ext - r.src;
+            } else {
+                const uint64_t ph = ((uintptr_t)in_map + so) & 15u;
+                x = ((x + 15u) & ~15ull) + ph;
+                runs.push_back(Run{so, x, ext});
+                m_din[k] = x;
+            }
+            x = m_din[k] + ext;
+            const uint64_t oph = ((uintptr_t)out_map + a.out_off[i]) & 15u;
+            y = ((y + 15u) & ~15ull) + oph;
+            m_dout[k] = y;
+            y += a.out_cap[i];
+            m_src[k] = so;
+            m_dst[k] = a.out_off[i];
+            m_in_len[k] = a.in_len[i];
+            m_cap[k] = a.out_cap[i];
+            const uint32_t l = a.compress ? a.in_len[i] : a.out_cap[i];
+            if (l > max_len) max_len = l;
+        }
+        uint8_t *d_in = (uint8_t *)sl.d_in.get(x + 16);
+        uint8_t *d_out = (uint8_t *)sl.d_out.get(y + 16);
+        uint8_t *d_meta = (uint8_t *)sl.d_meta.get((size_t)n * mrec);
+        const size_t res_off = (uint8_t *)(m_cap + n) - h_meta;
+        check(hipMemcpyAsync(d_meta, h_meta, res_off, hipMemcpyHostToDevice, sl.stream), "hipMemcpyAsync");
+        const uint64_t *d_src = (const uint64_t *)d_meta, *d_din = d_src + n, *d_dout = d_din + n,
+                       *d_dst = d_dout + n;
+        const uint32_t *d_in_len = (const uint32_t *)(d_dst + n), *d_cap = d_in_len + n;
+        uint32_t *d_out_len = (uint32_t *)(d_cap + n);
+        if (runs.size() <= 8u + n / 64u) {
+            for (const Run &r : runs)
+                if (r.len)
+                    check(hipMemcpyAsync(d_in + r.dst, a.in + r.src, r.len, hipMemcpyHostToDevice, sl.stream),
+                          "hipMemcpyAsync");
+        } else {
+            check(lzf_launch_move(in_map, d_src, d_in, d_din, d_in_len, min_len, n, sl.stream), "gather launch");
+        }
+        LzfBatch b{};
+        b.in = d_in;
+        b.in_off = d_din;
+        b.in_len = d_in_len;
+        b.out = d_out;
+        b.out_off = d_dout;
+        b.out_cap = d_cap;
+        b.out_len = d_out_len;
+        b.err = (int32_t *)(d_out_len + n);
+        b.count = n;
+        b.max_len = max_len;
+        check(launch(a, b, sl.stream), "kernel launch");
+        check(lzf_launch_move(d_out, d_dout, out_map, d_dst, d_out_len, 0u, n, sl.stream), "scatter launch");
+        check(hipMemcpyAsync(h_meta + res_off, d_meta + res_off, (size_t)n * mrec - res_off, hipMemcpyDeviceToHost,
+                             sl.stream),
+              "hipMemcpyAsync");
+        check(hipEventRecord(sl.done, sl.stream), "hipEventRecord");
+        sl.first = k0;
+        sl.count = n;
+        sl.busy = true;
+    }
+    drain(c.slot[round & 1u]);
+    drain(c.slot[(round + 1u) & 1u]);
+}
+
+/* the [lo, hi) byte ranges a sub-batch reads and writes in the caller's arenas */
+void spans(const HostArgs &a, const View &v, uintptr_t &ilo, uintptr_t &ihi, uintptr_t &olo, uintptr_t &ohi)
+{
+    ilo = olo = UINTPTR_MAX;
+    ihi = ohi = 0;
+    for (uint32_t k = 0; k < v.count; k++) {
+        const uint32_t i = v.at(k);
+        const uintptr_t s = (uintptr_t)a.in + a.in_off[i], d = (uintptr_t)a.out + a.out_off[i];
+        if (s < ilo) ilo = s;
+        if (s + in_extent(a, i) > ihi) ihi = s + in_extent(a, i);
+        if (d < olo) olo = d;
+        if (d + a.out_cap[i] > ohi) ohi = d + a.out_cap[i];
+    }
+    if (ihi < ilo) ihi = ilo;
+    if (ohi < olo) ohi = olo;
+}
+
+void host_batch(Ctx &c, const HostArgs &a, const View &v)
+{
+    DeviceGuard g(c.dev);
+    uintptr_t ilo, ihi, olo, ohi;
+    spans(a, v, ilo, ihi, olo, ohi);
+    if (is_registered(ilo, ihi) && is_registered(olo, ohi)) {
+        void *im = nullptr, *om = nullptr;
+        /* device addresses of the arenas' bases (the ranges are mapped) */
+        if (hipHostGetDevicePointer(&im, (void *)ilo, 0) == hipSuccess &&
+            hipHostGetDevicePointer(&om, (void *)olo, 0) == hipSuccess) {
+            host_batch_mapped(c, a, v, (const uint8_t *)im - (ilo - (uintptr_t)a.in),
+                              (uint8_t *)om - (olo - (uintptr_t)a.out));
+            return;
+        }
+        (void)hipGetLastError();
+    }
+    uint64_t sin = 0, sout = 0;
+    for (uint32_t k = 0; k < v.count; k++) {
+        const uint32_t i = v.at(k);
+        sin += in_extent(a, i) ? in_extent(a, i) : 1u;
+        sout += a.out_cap[i];
+    }
+    /* large batches whose outputs are not much bigger than their inputs go
+     * through the chunked pipeline */
+    const uint64_t chunk = 32ull << 20;
+    if (sin >= 2 * chunk && sout <= 4 * sin)
+        host_batch_staged(c, a, v, chunk, 4 * chunk);
+    else
+        host_batch_small(c, a, v);
+}
+
+/* a sub-batch on one context, failures as a return code */
+int host_run(Ctx &c, const HostArgs &a, const View &v)
+{
+    try {
+        host_batch(c, a, v);
+        return LZF_GPU_OK;
+    } catch (const LzfFail &f) {
+        c.quiesce();
+        return f.code;
+    }
+}
+
+/* ---- decoded sizes of host streams (the pre-pass of lzf_dsize.hip) -------- */
+
+void host_dsize(Ctx &c, const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, uint32_t *out_size,
+                int32_t *err, const View &v, uint32_t limit)
+{
+    DeviceGuard g(c.dev);
+    const uint32_t n = v.count;
+    uint64_t bin = 0;
+    for (uint32_t k = 0; k < n; k++) bin += in_len[v.at(k)] ? in_len[v.at(k)] : 1u;
+    const size_t mb = (size_t)n * (sizeof(uint64_t) + 3 * sizeof(uint32_t));
+    uint8_t *h_in = (uint8_t *)c.h_in.get(bin), *h_meta = (uint8_t *)c.h_meta.get(mb);
+    uint8_t *d_in = (uint8_t *)c.d_in.get(bin), *d_meta = (uint8_t *)c.d_meta.get(mb);
+    uint64_t *m_off = (uint64_t *)h_meta;
+    uint32_t *m_len = (uint32_t *)(m_off + n);
+    uint64_t x = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t i = v.at(k);
+        const uint32_t e = in_len[i] ? in_len[i] : 1u;     /* a 0-length stream reads 1 byte */
+        memcpy(h_in + x, in + in_off[i], e);
+        m_off[k] = x;
+        m_len[k] = in_len[i];
+        x += e;
+    }
+    const size_t res = (size_t)n * (sizeof(uint64_t) + sizeof(uint32_t));
+    check(hipMemcpyAsync(d_in, h_in, bin, hipMemcpyHostToDevice, c.stream), "hipMemcpyAsync");
+    check(hipMemcpyAsync(d_meta, h_meta, res, hipMemcpyHostToDevice, c.stream), "hipMemcpyAsync");
+    check(lzf_launch_dsize(d_in, (const uint64_t *)d_meta, (const uint32_t *)(d_meta + (size_t)n * sizeof(uint64_t)),
+                           (uint32_t *)(d_meta + res), (int32_t *)(d_meta + res + (size_t)n * sizeof(uint32_t)), n,
+                           limit, c.stream),
+          "kernel launch");
+    check(hipMemcpyAsync(h_meta + res, d_meta + res, mb - res, hipMemcpyDeviceToHost, c.stream), "hipMemcpyAsync");
+    check(hipStreamSynchronize(c.stream), "hipStreamSynchronize");
+    const uint32_t *r_size = (const uint32_t *)(h_meta + res);
+    const int32_t *r_err = (const int32_t *)(r_size + n);
+    for (uint32_t k = 0; k < n; k++) {
+        out_size[v.at(k)] = r_size[k];
+        err[v.at(k)] = r_err[k];
+    }
+}
+
+/* ---- the per-device workers ---------------------------------------------- */
+
+struct Worker {
+    int dev = 0;
+    int numa = -1;
+    bool bound = false;
+    bool ready = false;
+    std::unique_ptr<Ctx> ctx;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::function<void()>> q;
+    std::thread th;
+
+    explicit Worker(int d) : dev(d)
+    {
+        th = std::thread([this] { run(); });
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [this] { return ready; });
+    }
+    void run()
+    {
+        cpu_set_t local;
+        const int node = device_numa(dev, &local);
+        const bool b = bind_to_node(node, local);
+        (void)hipSetDevice(dev);
+        std::unique_ptr<Ctx> c(new Ctx(dev, b));
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            numa = node;
+            bound = b;
+            ctx = std::move(c);
+            ready = true;
+        }
+        cv.notify_all();
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [this] { return !q.empty(); });
+                f = std::move(q.front());
+                q.pop_front();
+            }
+            f();
+        }
+    }
+    void post(std::function<void()> f)
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            q.push_back(std::move(f));
+        }
+        cv.notify_all();
+    }
+};
+
+/* one worker per plan entry, made on first use and kept for the process's
+ * life (its thread waits on its queue; process exit ends it) */
+std::vector<Worker *> &workers()
+{
+    static std::mutex mu;
+    static std::vector<Worker *> w;
+    std::lock_guard<std::mutex> lk(mu);
+    if (w.empty())
+        for (int d : plan().dev) w.push_back(new Worker(d));
+    return w;
+}
+
+/* completion of the entries of one call */
+struct Join {
+    std::mutex mu;
+    std::condition_variable cv;
+    uint32_t left = 0;
+    int rc = LZF_GPU_OK;
+    void done(int r)
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (r != LZF_GPU_OK && rc == LZF_GPU_OK) rc = r;
+        if (--left == 0) cv.notify_all();
+    }
+    int wait()
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [this] { return left == 0; });
+        return rc;
+    }
+};
+
+struct Spread {
+    uint32_t values = 0;
+    double ms = 0;
+};
+thread_local std::vector<Spread> g_spread;
+
+/* Run job(ctx, view) for every plan entry's share of `count` values (value i
+ * to entry i mod G) on the entries' workers, or on the calling thread when
+ * there is one entry or one value. */
+int dispatch(uint32_t count, const std::function<int(Ctx &, const View &)> &job)
+{
+    const Plan &P = plan();
+    if (P.rc != LZF_GPU_OK) return P.rc;
+    const uint32_t G = (uint32_t)P.dev.size();
+    g_spread.assign(G, Spread{});
+    if (G <= 1 || count == 1) {
+        const auto t0 = std::chrono::steady_clock::now();
+        int rc;
+        try {
+            rc = job(caller_ctx(), View{0, 1, count});
+        } catch (const LzfFail &f) {
+            rc = f.code;
+        }
+        g_spread[0].values = count;
+        g_spread[0].ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        return rc;
+    }
+    std::vector<Worker *> &w = workers();
+    Join j;
+    j.left = G;
+    for (uint32_t d = 0; d < G; d++) {
+        View v;
+        v.count = lzf_host_split(count, G, d, &v.first, &v.stride);
+        g_spread[d].values = v.count;
+        if (!v.count || !w[d]->ctx->ok) {
+            j.done(v.count ? LZF_GPU_ENODEV : LZF_GPU_OK);
+            continue;
+        }
+        Spread *sp = &g_spread[d];
+        Ctx *c = w[d]->ctx.get();
+        w[d]->post([&j, &job, c, v, sp] {
+            const auto t0 = std::chrono::steady_clock::now();
+            int rc;
+            try {
+                rc = job(*c, v);
+            } catch (const LzfFail &f) {
+                rc = f.code;
+            }
+            sp->ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            j.done(rc);
+        });
+    }
+    return j.wait();
+}
+
+int host_batch_call(const HostArgs &a, uint32_t count)
+{
+    if (!count || !a.in || !a.in_off || !a.in_len || !a.out || !a.out_off || !a.out_cap || !a.out_len)
+        return LZF_GPU_EARG;
+    return dispatch(count, [&a](Ctx &c, const View &v) { return host_run(c, a, v); });
+}
+
+}  // namespace
+
+extern "C" {
+
+/* Single calls are batches of one, on the calling thread's context (the
+ * plan's first device).  A failure of the device path (no usable gfx950, a
+ * HIP error) is reported, never aborted on: lzf_compress returns 0, which the
+ * caller already reads as "store the value plain" (src/query.c:393-397);
+ * lzf_decompress returns 0 with errno EIO, an errno the reference codec never
+ * sets (src/lzf.h:85-91 lists E2BIG and EINVAL). */
+unsigned int lzf_compress(const void *const in_data, unsigned int in_len, void *out_data, unsigned int out_len)
+{
+    if (!in_len || !out_len) return 0;                    /* src/lzf_c.c:131 */
+    if (!in_data || !out_data) return 0;
+    uint64_t zero = 0;
+    uint32_t res = 0;
+    const HostArgs a{true, (const uint8_t *)in_data, &zero, &in_len, (uint8_t *)out_data, &zero, &out_len, &res,
+                     nullptr};
+    return host_batch_call(a, 1) == LZF_GPU_OK ? res : 0u;
+}
+
+unsigned int lzf_decompress(const void *const in_data, unsigned int in_len, void *out_data, unsigned int out_len)
+{
+    uint8_t none = 0;
+    if (!in_data || (!out_data && out_len)) {             /* the reference would fault */
+        errno = EINVAL;
+        return 0;
+    }
+    if (!out_data) out_data = &none;                      /* out_len 0: nothing is written */
+    uint64_t zero = 0;
+    uint32_t res = 0;
+    int32_t err = 0;
+    const HostArgs a{false, (const uint8_t *)in_data, &zero, &in_len, (uint8_t *)out_data, &zero, &out_len, &res,
+                     &err};
+    if (host_batch_call(a, 1) != LZF_GPU_OK) {
+        errno = EIO;
+        return 0;
+    }
+    if (!res) errno = err ? err : EINVAL;
+    return res;
+}
+
+int lzf_host_compress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, uint8_t *out,
+                            const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len, uint32_t count)
+{
+    return host_batch_call(HostArgs{true, in, in_off, in_len, out, out_off, out_cap, out_len, nullptr}, count);
+}
+
+int lzf_host_decompress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, uint8_t *out,
+                              const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len, int32_t *err,
+                              uint32_t count)
+{
+    if (!err) return LZF_GPU_EARG;
+    return host_batch_call(HostArgs{false, in, in_off, in_len, out, out_off, out_cap, out_len, err}, count);
+}
+
+int lzf_host_decoded_size_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                                uint32_t *out_size, int32_t *err, uint32_t count, uint32_t out_limit)
+{
+    if (!count || !in || !in_off || !in_len || !out_size || !err) return LZF_GPU_EARG;
+    return dispatch(count, [=](Ctx &c, const View &v) {
+        try {
+            host_dsize(c, in, in_off, in_len, out_size, err, v, out_limit);
+            return LZF_GPU_OK;
+        } catch (const LzfFail &f) {
+            c.quiesce();
+            return f.code;
+        }
+    });
+}
+
+int lzf_host_register(const void *ptr, uint64_t len)
+{
+    if (!ptr || !len) return LZF_GPU_EARG;
+    const uintptr_t lo = (uintptr_t)ptr, hi = lo + len;
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        auto it = g_reg.upper_bound(lo);
+        if (it != g_reg.end() && it->first < hi) return LZF_GPU_EARG;          /* overlaps a later range */
+        if (it != g_reg.begin() && std::prev(it)->second > lo) return LZF_GPU_EARG;
+    }
+    const Plan &P = plan();
+    if (P.rc != LZF_GPU_OK) return P.rc;
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(P.dev[0]) != hipSuccess) return LZF_GPU_ENODEV;
+    /* portable: every device of the plan maps it */
+    const hipError_t e = hipHostRegister((void *)ptr, len, hipHostRegisterMapped | hipHostRegisterPortable);
+    if (prev >= 0 && prev != P.dev[0]) (void)hipSetDevice(prev);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return code_of(e);
+    }
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg[lo] = hi;
+    return LZF_GPU_OK;
+}
+
+int lzf_host_unregister(const void *ptr)
+{
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        auto it = g_reg.find((uintptr_t)ptr);
+        if (it == g_reg.end()) return LZF_GPU_EARG;
+        g_reg.erase(it);
+    }
+    return hipHostUnregister((void *)ptr) == hipSuccess ? LZF_GPU_OK : LZF_GPU_ELAUNCH;
+}
+
+int lzf_gpu_parse_device_list(const char *spec, int visible, int *dev, int max)
+{
+    if (!spec || !dev || max <= 0) return LZF_GPU_EARG;
+    if (!strcmp(spec, "all")) {
+        int n = 0;
+        for (int d = 0; d < visible && n < max; d++) dev[n++] = d;
+        return n > 0 ? n : LZF_GPU_ENODEV;
+    }
+    int n = 0;
+    const char *s = spec;
+    while (*s) {
+        while (*s == ' ') s++;
+        char *end;
+        const long d = strtol(s, &end, 10);
+        if (end == s || d < 0 || d >= visible || n >= max) return end == s || n >= max ? LZF_GPU_EARG : LZF_GPU_ENODEV;
+        dev[n++] = (int)d;
+        s = end;
+        while (*s == ' ') s++;
+        if (*s == ',') s++;
+        else if (*s) return LZF_GPU_EARG;
+    }
+    return n > 0 ? n : LZF_GPU_EARG;
+}
+
+uint32_t lzf_host_split(uint32_t count, uint32_t groups, uint32_t g, uint32_t *first, uint32_t *stride)
+{
+    if (first) *first = g;
+    if (stride) *stride = groups ? groups : 1u;
+    if (!groups || g >= groups || g >= count) return 0;
+    return (count - g + groups - 1u) / groups;
+}
+
+int lzf_gpu_device_plan(int *device, int *numa_node, int *bound, int max)
+{
+    const Plan &P = plan();
+    if (P.rc != LZF_GPU_OK) return P.rc;
+    const int G = (int)P.dev.size();
+    if (G > 1) {
+        std::vector<Worker *> &w = workers();
+        for (int k = 0; k < G && k < max; k++) {
+            if (device) device[k] = w[k]->dev;
+            if (numa_node) numa_node[k] = w[k]->numa;
+            if (bound) bound[k] = w[k]->bound ? 1 : 0;
+        }
+    } else if (max > 0) {
+        cpu_set_t local;
+        if (device) device[0] = P.dev[0];
+        if (numa_node) numa_node[0] = device_numa(P.dev[0], &local);
+        if (bound) bound[0] = 0;                           /* the calling thread is the caller's */
+    }
+    return G;
+}
+
+int lzf_host_last_spread(uint32_t *values, double *ms, int max)
+{
+    const int G = (int)g_spread.size();
+    for (int k = 0; k < G && k < max; k++) {
+        if (values) values[k] = g_spread[k].values;
+        if (ms) ms[k] = g_spread[k].ms;
+    }
+    return G;
+}
+
+void lzf_gpu_release(void)
+{
+    lzf_scratch_release_all();
+    try {
+        caller_ctx().release();
+    } catch (const LzfFail &) {
+    }
+    if (plan().rc == LZF_GPU_OK && plan().dev.size() > 1) {
+        std::vector<Worker *> &w = workers();
+        Join j;
+        j.left = (uint32_t)w.size();
+        for (Worker *x : w)
+            x->post([&j, x] {
+                x->ctx->release();
+                j.done(LZF_GPU_OK);
+            });
+        j.wait();
+    }
+}
+
+}  // extern "C"

@@ -103,6 +103,17 @@ hipError_t lzf_launch_frame(LzfFrameArgs &a, hipStream_t s,
 size_t lzf_frame_work_bytes(uint32_t count);
 void lzf_frame_carve(LzfFrameArgs &a, void *work);
 const char *lzf_compress_kernel_name(void);
+/* value moves between mapped host memory and device arenas (lzf_hostio.hip):
+ * len[k] (at least min_len) bytes from src + src_off[k] to dst + dst_off[k] */
+hipError_t lzf_launch_move(const uint8_t *src, const uint64_t *src_off, uint8_t *dst, const uint64_t *dst_off,
+                           const uint32_t *len, uint32_t min_len, uint32_t count, hipStream_t s);
+/* lzf_api.cpp, for the host-memory paths of lzf_host.cpp: the routed
+ * launches, the routing's batch threshold, the device check, the scratch */
+hipError_t lzf_route_compress(const LzfBatch &b, hipStream_t s);
+hipError_t lzf_route_decompress(const LzfBatch &b, hipStream_t s);
+uint32_t lzf_route_min_count(uint32_t max_len);
+bool lzf_device_ok(int dev);
+void lzf_scratch_release_all(void);
 const char *lzf_decompress_kernel_name(void);
 
 #endif

@@ -31,6 +31,12 @@ EXPORTS = (
     "lzf_gpu_kv_frame_work_size",
     "lzf_gpu_kv_frame",
     "lzf_gpu_release",
+    "lzf_host_register",
+    "lzf_host_unregister",
+    "lzf_gpu_device_plan",
+    "lzf_host_last_spread",
+    "lzf_host_split",
+    "lzf_gpu_parse_device_list",
 )
 
 # item encodings (src/net.h:274-278) and the MGET reply code (src/query.h:71)
@@ -119,6 +125,18 @@ def _load(path):
     L.lzf_gpu_kv_frame.restype = ctypes.c_int
     L.lzf_gpu_kv_frame.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, ctypes.c_int,
                                    vp, u64, vp, vp, vp]
+    L.lzf_host_register.restype = ctypes.c_int
+    L.lzf_host_register.argtypes = [vp, u64]
+    L.lzf_host_unregister.restype = ctypes.c_int
+    L.lzf_host_unregister.argtypes = [vp]
+    L.lzf_gpu_device_plan.restype = ctypes.c_int
+    L.lzf_gpu_device_plan.argtypes = [vp, vp, vp, ctypes.c_int]
+    L.lzf_host_last_spread.restype = ctypes.c_int
+    L.lzf_host_last_spread.argtypes = [vp, vp, ctypes.c_int]
+    L.lzf_host_split.restype = u32
+    L.lzf_host_split.argtypes = [u32, u32, u32, vp, vp]
+    L.lzf_gpu_parse_device_list.restype = ctypes.c_int
+    L.lzf_gpu_parse_device_list.argtypes = [ctypes.c_char_p, ctypes.c_int, vp, ctypes.c_int]
     del i32
     _LOADED[path] = L
     return L
@@ -235,6 +253,45 @@ def host_decompress_batch(inp, in_off, in_len, out, out_off, out_cap, out_len, e
                                          _np_ptr(out), _np_ptr(out_off), _np_ptr(out_cap),
                                          _np_ptr(out_len), _np_ptr(err), len(in_len))
     _check(rc, "lzf_host_decompress_batch")
+
+
+def host_register(arr):
+    """lzf_host_register over a numpy array's bytes: the host batches whose
+    arenas lie in registered ranges move values without CPU copies."""
+    _check(lib().lzf_host_register(_np_ptr(arr), arr.nbytes), "lzf_host_register")
+
+
+def host_unregister(arr):
+    _check(lib().lzf_host_unregister(_np_ptr(arr)), "lzf_host_unregister")
+
+
+def device_plan():
+    """[(device, numa_node, bound)] of the host-memory calls (LZF_GPU_DEVICES)."""
+    d, n, b = (ctypes.c_int * 64)(), (ctypes.c_int * 64)(), (ctypes.c_int * 64)()
+    g = lib().lzf_gpu_device_plan(d, n, b, 64)
+    if g < 0:
+        raise RuntimeError(f"lzf_gpu_device_plan failed: {_ERRS.get(g, g)}")
+    return [(d[k], n[k], bool(b[k])) for k in range(g)]
+
+
+def host_last_spread():
+    """[(values, ms)] per plan entry of this thread's last host-memory call."""
+    v, t = (ctypes.c_uint32 * 64)(), (ctypes.c_double * 64)()
+    g = lib().lzf_host_last_spread(v, t, 64)
+    return [(v[k], t[k]) for k in range(min(g, 64))]
+
+
+def host_split(count, groups, g):
+    """(first, stride, n): the values entry g of ``groups`` takes."""
+    f, s = ctypes.c_uint32(), ctypes.c_uint32()
+    n = lib().lzf_host_split(count, groups, g, ctypes.byref(f), ctypes.byref(s))
+    return f.value, s.value, n
+
+
+def parse_device_list(spec, visible):
+    out = (ctypes.c_int * 64)()
+    n = lib().lzf_gpu_parse_device_list(spec.encode(), visible, out, 64)
+    return list(out[:n]) if n > 0 else n
 
 
 def kv_frame(keys, key_off, key_len, vals, val_off, val_size, enc, val_len, elements,

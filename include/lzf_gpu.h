@@ -96,9 +96,21 @@ int lzf_gpu_synth_fill(int kind, uint64_t seed, uint64_t first, uint64_t stride,
 
 /*
  * Host-memory batch (the north star's PCIe-inclusive path): the same as the
- * device calls, but every pointer is host memory.  The library stages
- * through pinned buffers and hipMemcpyAsync on its own stream and returns
- * after the results are back in host memory.
+ * device calls, but every pointer is host memory, and the call returns after
+ * the results are back in host memory.
+ *
+ * Devices: with LZF_GPU_DEVICES set ("0,1,2,3", "all"; an index may repeat),
+ * value i goes to entry i mod G of that list, each entry served by its own
+ * worker thread (bound to its device's NUMA node), streams and staging; the
+ * results land at index i.  A failure on any entry makes the call return
+ * that entry's LZF_GPU_E* code.  Unset: the one device LZF_GPU_DEVICE
+ * (default 0), on the calling thread.
+ *
+ * Moving bytes: when both arenas' spans lie in ranges given to
+ * lzf_host_register, no CPU copies a value byte (the GPU and its DMA engines
+ * move them; the bytes of an output slot past out_len[i] are then
+ * unspecified, as after a failed call).  Otherwise the library stages values
+ * through its own pinned buffers.  Results are identical either way.
  */
 int lzf_host_compress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
                             uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
@@ -106,6 +118,35 @@ int lzf_host_compress_batch(const uint8_t *in, const uint64_t *in_off, const uin
 int lzf_host_decompress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
                               uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
                               uint32_t *out_len, int32_t *err, uint32_t count);
+
+/*
+ * Register [ptr, ptr+len) of caller memory (an arena of request buffers, the
+ * store's values) for the host-memory batches: page-locked and mapped into
+ * every device of the plan (hipHostRegister, portable + mapped).  The range
+ * must stay allocated until lzf_host_unregister(ptr).  Returns LZF_GPU_OK,
+ * LZF_GPU_EARG (NULL, empty, or overlapping a registered range) or the HIP
+ * failure's code.  Registration costs about 15 ms per GiB (measured).
+ */
+int lzf_host_register(const void *ptr, uint64_t len);
+int lzf_host_unregister(const void *ptr);
+
+/*
+ * The device plan of the host-memory calls: returns G, the number of
+ * entries, and fills (for k < max) device[k] (HIP device index),
+ * numa_node[k] (the device's node from sysfs, -1 unknown) and bound[k]
+ * (1 when entry k's worker thread runs on that node's CPUs with its memory
+ * preferred there).  A negative LZF_GPU_E* code when the plan is invalid.
+ */
+int lzf_gpu_device_plan(int *device, int *numa_node, int *bound, int max);
+/* The calling thread's last host-memory call: values each plan entry took
+ * and its wall time in ms (the per-device spread).  Returns G. */
+int lzf_host_last_spread(uint32_t *values, double *ms, int max);
+/* The partition rule: entry g of `groups` takes values first + k * stride,
+ * k < the returned count (first = g, stride = groups). */
+uint32_t lzf_host_split(uint32_t count, uint32_t groups, uint32_t g, uint32_t *first, uint32_t *stride);
+/* The LZF_GPU_DEVICES grammar ("all", or comma-separated indices below
+ * `visible`): fills dev[] and returns the count, or a negative code. */
+int lzf_gpu_parse_device_list(const char *spec, int visible, int *dev, int max);
 
 /*
  * MGET / KEYS reply assembled on the device.
@@ -144,9 +185,9 @@ int lzf_gpu_kv_frame(const uint8_t *keys, const uint64_t *key_off, const uint32_
                      uint8_t *frame, uint64_t max_response, uint64_t *frame_len, void *work,
                      void *stream);
 
-/* Free the library's device scratch (all devices) and the calling thread's
- * staging buffers; later calls allocate them again.  Each thread's staging
- * buffers are also freed when the thread exits. */
+/* Free the library's device scratch (all devices), the calling thread's and
+ * the device workers' staging buffers; later calls allocate them again.
+ * Each thread's staging buffers are also freed when the thread exits. */
 void lzf_gpu_release(void);
 
 /* One-time self-check of the current device (run lazily before the first

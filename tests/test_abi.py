@@ -64,7 +64,8 @@ def _kernels(path):
 ROUTED = {"lzf_cand_stream_kernel", "lzf_parse_lane_kernel", "lzf_cand_table_kernel", "lzf_parse_rec_kernel",
           "lzf_compress_window_kernel", "lzf_decompress_pipe_kernel", "lzf_decompress_tokpar_kernel",
           "lzf_dsize_kernel", "lzf_lds_order_probe_kernel", "lzf_synth_kernel", "lzf_frame_size_kernel",
-          "lzf_frame_scan_kernel", "lzf_frame_write_kernel", "lzf_frame_check_kernel"}
+          "lzf_frame_scan_kernel", "lzf_frame_write_kernel", "lzf_frame_check_kernel",
+          "lzf_move_kernel"}
 # cross-check forms: the diagnostic build only
 DIAG_ONLY = {"lzf_wparse_kernel", "lzf_cand_q1_kernel", "lzf_cand_small_kernel", "lzf_cand_ring_kernel",
              "lzf_cand_mid_kernel", "lzf_compress_serial_kernel", "lzf_decompress_serial_kernel",
@@ -124,3 +125,14 @@ def test_batch_calls_reject_bad_arguments_without_device():
     assert L.lzf_gpu_synth_fill(0, 0, 0, 1, 0, 16, p, null) == -1
     assert L.lzf_host_compress_batch(null, p, p, p, p, p, p, 1) == -1
     assert L.lzf_host_decompress_batch(p, p, p, p, p, p, p, null, 0) == -1
+
+
+def test_batch_calls_reject_bad_arguments_host_extensions():
+    import ctypes
+    L = gibson_amd.lib()
+    null = ctypes.c_void_p(0)
+    assert L.lzf_host_register(null, 64) == -1
+    buf = ctypes.create_string_buffer(64)
+    assert L.lzf_host_register(ctypes.cast(buf, ctypes.c_void_p), 0) == -1
+    assert L.lzf_host_unregister(ctypes.cast(buf, ctypes.c_void_p)) == -1     # never registered
+    assert L.lzf_host_decoded_size_batch(null, null, null, null, null, 0, 16) == -1

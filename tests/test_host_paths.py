@@ -1,0 +1,190 @@
+"""The host-memory batch calls on the GPU: registered arenas (no CPU byte
+copies, lzf_host_register) against the staged path and the oracle, and the
+multi-device plan (LZF_GPU_DEVICES) inside the library -- value i to plan
+entry i mod G, each entry a worker thread with its own streams and staging --
+run as two contexts on the box's one device ("0,0"), bit-exact against the
+oracle and the reference's configs[1] digest."""
+import json
+import os
+import random
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from tests.oracle_lib import ROOT, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _aligned(nbytes):
+    raw = np.zeros(nbytes + 8192, np.uint8)
+    k = (-raw.ctypes.data) % 4096
+    return raw[k:k + nbytes]
+
+
+@pytest.fixture
+def registered():
+    import gibson_amd
+    held = []
+
+    def reg(a):
+        gibson_amd.host_register(a)
+        held.append(a)
+        return a
+    yield reg
+    for a in held:
+        gibson_amd.host_unregister(a)
+
+
+def test_registered_matches_staged_and_oracle(oracle, registered):
+    # shuffled, unaligned arena order with mixed sizes (0 B .. 20 KiB): the
+    # GPU gathers the values from the mapped arena and scatters the streams
+    import gibson_amd
+    rnd = random.Random(31)
+    count = 6000
+    sizes = [rnd.choice([4096, 4096, rnd.randint(0, 20000)]) for _ in range(count)]
+    order = list(range(count))
+    rnd.shuffle(order)
+    pos, offs = 0, [0] * count
+    for i in order:
+        offs[i] = pos
+        pos += sizes[i] + rnd.randint(0, 3)
+    arena = registered(_aligned(pos + 16))
+    for i in range(count):
+        arena[offs[i]:offs[i] + sizes[i]] = np.frombuffer(synth(i % 6, 0x5EED00B1, i, sizes[i]), np.uint8)
+    off = np.array(offs, dtype=np.uint64)
+    ln = np.array(sizes, dtype=np.uint32)
+    cap = np.maximum(ln.astype(np.int64) - 4, 0).astype(np.uint32)
+    out_r = registered(_aligned(pos + 16))
+    olen_r = np.zeros(count, np.uint32)
+    gibson_amd.host_compress_batch(arena, off, ln, out_r, off, cap, olen_r)
+    # the same batch staged (an unregistered output arena)
+    out_s = np.zeros(pos + 16, np.uint8)
+    olen_s = np.zeros(count, np.uint32)
+    gibson_amd.host_compress_batch(arena, off, ln, out_s, off, cap, olen_s)
+    assert np.array_equal(olen_r, olen_s)
+    for i in range(count):
+        got = bytes(out_r[offs[i]:offs[i] + olen_r[i]]) if olen_r[i] else None
+        assert got == (bytes(out_s[offs[i]:offs[i] + olen_s[i]]) if olen_s[i] else None), i
+    for i in rnd.sample(range(count), 600):
+        v = bytes(arena[offs[i]:offs[i] + sizes[i]])
+        exp = oracle.compress(v, int(cap[i])) if sizes[i] and cap[i] else None
+        got = bytes(out_r[offs[i]:offs[i] + olen_r[i]]) if olen_r[i] else None
+        assert got == exp, i
+    ok = olen_r > 0
+    dec = registered(_aligned(pos + 16))
+    dl = np.zeros(int(ok.sum()), np.uint32)
+    er = np.zeros(int(ok.sum()), np.int32)
+    gibson_amd.host_decompress_batch(out_r, off[ok], olen_r[ok], dec, off[ok], ln[ok], dl, er)
+    assert (dl == ln[ok]).all() and (er == 0).all()
+    for i in np.nonzero(ok)[0]:
+        assert bytes(dec[offs[i]:offs[i] + sizes[i]]) == bytes(arena[offs[i]:offs[i] + sizes[i]]), i
+
+
+def test_registered_contiguous_runs_and_exact_writes(oracle, registered):
+    # values back to back (the DMA engines copy whole runs) and output slots
+    # with guard bytes between them: the scatter writes exactly out_len bytes
+    import gibson_amd
+    count, n = 4096, 4096
+    arena = registered(_aligned(count * n))
+    for i in range(count):
+        arena[i * n:(i + 1) * n] = np.frombuffer(synth(i % 6, 0x5EED00B2, i, n), np.uint8)
+    off = np.arange(count, dtype=np.uint64) * n
+    ln = np.full(count, n, np.uint32)
+    cap = np.full(count, n - 4, np.uint32)
+    slot = n + 64
+    out = registered(_aligned(count * slot))
+    out[:] = 0xA5
+    oof = np.arange(count, dtype=np.uint64) * slot
+    olen = np.zeros(count, np.uint32)
+    gibson_amd.host_compress_batch(arena, off, ln, out, oof, cap, olen)
+    for i in range(count):
+        s = out[i * slot:(i + 1) * slot]
+        exp = oracle.compress(bytes(arena[i * n:(i + 1) * n]), n - 4)
+        if exp is None:
+            assert olen[i] == 0
+        else:
+            assert bytes(s[:olen[i]]) == exp, i
+            assert (s[olen[i]:] == 0xA5).all(), i
+
+
+def test_registered_decode_errors_and_empty_streams(oracle, registered):
+    # decoder errno parity through the registered path: truncated and
+    # corrupted streams, and 0-length streams (which read one control byte)
+    import gibson_amd
+    rnd = random.Random(5)
+    streams, caps, exp = [], [], []
+    for k in range(300):
+        v = synth(k % 6, 0x5EED00B3, k, rnd.randint(1, 9000))
+        s = oracle.compress(v, len(v) + len(v) // 16 + 64)
+        if k % 3 == 1:
+            s = s[:rnd.randint(0, len(s))]
+        elif k % 3 == 2:
+            b = bytearray(s)
+            b[rnd.randrange(len(b))] ^= 0xFF
+            s = bytes(b)
+        c = len(v) if k % 5 else len(v) // 2
+        streams.append(s)
+        caps.append(c)
+        exp.append(oracle.decompress(s, c))
+    pos, offs = 0, []
+    for s in streams:
+        offs.append(pos)
+        pos += len(s) + 1
+    inp = registered(_aligned(pos + 16))
+    for s, o in zip(streams, offs):
+        inp[o:o + len(s)] = np.frombuffer(s, np.uint8)
+        inp[o + len(s)] = 0xFF
+    doff, p = [], 0
+    for c in caps:
+        doff.append(p)
+        p += c + 7
+    out = registered(_aligned(p + 16))
+    dl = np.zeros(len(streams), np.uint32)
+    er = np.zeros(len(streams), np.int32)
+    gibson_amd.host_decompress_batch(inp, np.array(offs, np.uint64), np.array([len(s) for s in streams], np.uint32),
+                                     out, np.array(doff, np.uint64), np.array(caps, np.uint32), dl, er)
+    for k, (d, e) in enumerate(exp):
+        if d is None:
+            assert dl[k] == 0 and er[k] == e, k
+        else:
+            assert er[k] == 0 and bytes(out[doff[k]:doff[k] + dl[k]]) == d, k
+
+
+def test_register_rejects_overlap():
+    import gibson_amd
+    a = _aligned(1 << 20)
+    gibson_amd.host_register(a)
+    try:
+        with pytest.raises(RuntimeError):
+            gibson_amd.host_register(a[4096:8192])
+    finally:
+        gibson_amd.host_unregister(a)
+
+
+def test_two_contexts_on_one_device_bit_exact(digests_full):
+    # LZF_GPU_DEVICES=0,0: the round-robin split over two worker contexts,
+    # staged and registered, against the oracle and configs[1]'s digest
+    env = dict(os.environ, LZF_GPU_DEVICES="0,0")
+    env.pop("LZF_GPU_LANE_MIN", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "host_devices_run.py")], env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert [p[0] for p in res["plan"]] == [0, 0]
+    want = digests_full[(1, 0x5EED0002, 4096, 262144)]
+    for tag in ("staged", "registered"):
+        m = res["mixed_" + tag]
+        assert m["mismatches"] == 0 and m["roundtrip"], (tag, m)
+        assert [s[0] for s in m["spread"]] == [1500, 1500], m["spread"]
+        c = res["config1_" + tag]
+        assert c["digest"] == want, tag
+        assert [s[0] for s in c["spread"]] == [131072, 131072]
+
+
+@pytest.fixture(scope="module")
+def digests_full():
+    with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+        return {(d["kind"], d["seed"], d["n"], d["count"]): d["sha256"] for d in json.load(f)["digests"]}
