@@ -174,13 +174,15 @@ enum ScratchUser { SU_LANE = 0, SU_TABLE = 1, SU_WTAB = 2 };
 /* chunks of this thread's last scratch-bound compress launch (kernel_info) */
 thread_local uint32_t g_last_chunks = 0;
 
-hipError_t lane_compress(const LzfBatch &b, hipStream_t s, ScratchUser who)
+/* own: a caller's private scratch (the host pipelines' slots, so their
+ * chunks' compress launches can run side by side), else the device's */
+hipError_t lane_compress(const LzfBatch &b, hipStream_t s, ScratchUser who, Scratch *own = nullptr)
 {
     const bool table = who == SU_TABLE;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    Scratch &S = g_scratch[dev & 63];
+    Scratch &S = own ? *own : g_scratch[dev & 63];
     std::lock_guard<std::mutex> lk(S.mu);
 #ifdef LZF_DIAG
     const size_t per = who == SU_WTAB ? lzf_wtab_scratch_per_value(b.max_len)
@@ -268,7 +270,10 @@ uint32_t lane_min_count(uint32_t max_len)
     return 28672u;
 }
 
-hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
+/* bulk: the caller runs several launches side by side (the host-memory
+ * pipeline), so the per-launch floor of the parse overlaps and the batch
+ * threshold below which window64 wins alone does not apply */
+hipError_t launch_compress(const LzfBatch &b, hipStream_t s, Scratch *own = nullptr, bool bulk = false)
 {
     const KernelGen g = kernel_gen();
     if (g != GEN_WINDOW && g != GEN_SERIAL && !lds_order_ok()) return lzf_launch_compress(b, s);
@@ -297,12 +302,12 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s)
          * most LANE_DEFAULT_MAX bytes take the lane generation (the stream
          * cand kernel, lzf_stream.hip, and the lane parse), larger ones the
          * table generation (two-link records, lzf_cand.hip) */
-        if (b.count < lane_min_count(b.max_len) || !lzf_table_compress_supported(b.max_len))
+        if ((!bulk && b.count < lane_min_count(b.max_len)) || !lzf_table_compress_supported(b.max_len))
             return lzf_launch_compress(b, s);
         /* the lane generation where its kernel 1 takes the batch (a
          * diagnostic LZF_GPU_CAND=small stops at 4 KiB), else the table one */
         return lane_compress(b, s, b.max_len <= LANE_DEFAULT_MAX && lzf_lane_compress_supported(b.max_len)
-                                       ? SU_LANE : SU_TABLE);
+                                       ? SU_LANE : SU_TABLE, own);
     }
 }
 
@@ -346,6 +351,29 @@ hipError_t lzf_route_compress(const LzfBatch &b, hipStream_t s) { return launch_
 hipError_t lzf_route_decompress(const LzfBatch &b, hipStream_t s) { return launch_decompress(b, s); }
 uint32_t lzf_route_min_count(uint32_t max_len) { return lane_min_count(max_len); }
 bool lzf_device_ok(int dev) { return device_ok(dev); }
+hipError_t lzf_route_compress_bulk(const LzfBatch &b, hipStream_t s, void *scratch)
+{
+    return launch_compress(b, s, (Scratch *)scratch, true);
+}
+void *lzf_scratch_create(void) { return new Scratch(); }
+void lzf_scratch_destroy(void *scratch)
+{
+    Scratch *S = (Scratch *)scratch;
+    if (!S) return;
+    {
+        std::lock_guard<std::mutex> lk(S->mu);
+        scratch_free(*S);
+        if (S->ev) (void)hipEventDestroy(S->ev);
+    }
+    delete S;
+}
+void lzf_scratch_release(void *scratch)
+{
+    Scratch *S = (Scratch *)scratch;
+    if (!S) return;
+    std::lock_guard<std::mutex> lk(S->mu);
+    scratch_free(*S);
+}
 void lzf_scratch_release_all(void)
 {
     for (Scratch &S : g_scratch) {

@@ -240,9 +240,12 @@ struct Slot {
     hipEvent_t done = nullptr;
     Buf d_in, d_out, d_meta;
     Buf h_in{nullptr, 0, true}, h_out{nullptr, 0, true}, h_meta{nullptr, 0, true};
+    void *scratch = nullptr;       /* the slot's own compress scratch (registered path) */
+    hipEvent_t in_done = nullptr;  /* the chunk's inputs are on the device (registered path) */
     uint32_t first = 0, count = 0;
     bool busy = false;
 };
+constexpr uint32_t NSLOT = 3;      /* registered path: chunks in flight */
 
 struct Ctx {
     int dev = 0;
@@ -251,7 +254,7 @@ struct Ctx {
     hipStream_t stream = nullptr;
     Buf d_in, d_out, d_meta;
     Buf h_in{nullptr, 0, true}, h_out{nullptr, 0, true}, h_meta{nullptr, 0, true};
-    Slot slot[2];
+    Slot slot[NSLOT];
     Ctx(int device, bool bound) : dev(device), numa_bound(bound)
     {
         int n = 0;
@@ -281,6 +284,7 @@ struct Ctx {
         for (auto &sl : slot) {
             if (sl.stream) (void)hipStreamSynchronize(sl.stream);
             for (Buf *b : {&sl.d_in, &sl.d_out, &sl.d_meta, &sl.h_in, &sl.h_out, &sl.h_meta}) b->release();
+            lzf_scratch_release(sl.scratch);
             sl.busy = false;
         }
         for (Buf *b : {&d_in, &d_out, &d_meta, &h_in, &h_out, &h_meta}) b->release();
@@ -297,7 +301,11 @@ struct Ctx {
         }
         (void)hipGetLastError();
     }
-    ~Ctx() { release(); }
+    ~Ctx()
+    {
+        release();
+        for (auto &sl : slot) lzf_scratch_destroy(sl.scratch);
+    }
 };
 
 /* the calling thread's context, on the plan's first device */
@@ -385,6 +393,8 @@ void make_slot_streams(Ctx &c)
     for (auto &sl : c.slot) {
         if (!sl.stream) check(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking), "hipStreamCreate");
         if (!sl.done) check(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming), "hipEventCreate");
+        if (!sl.scratch) sl.scratch = lzf_scratch_create();
+        if (!sl.in_done) check(hipEventCreateWithFlags(&sl.in_done, hipEventDisableTiming), "hipEventCreate");
         sl.busy = false;
     }
 }
@@ -431,7 +441,7 @@ void host_batch_staged(Ctx &c, const HostArgs &a, const View &v, uint64_t chunk_
             if (l > max_len) max_len = l;
             k1++;
         }
-        Slot &sl = c.slot[round & 1u];
+        Slot &sl = c.slot[round & 1u];      /* two slots: CPU packing is the bound */
         drain(sl);
         const uint32_t n = k1 - k0;
         uint8_t *h_in = (uint8_t *)sl.h_in.get(bin);
@@ -567,38 +577,51 @@ void host_batch_small(Ctx &c, const HostArgs &a, const View &v)
 }
 
 /* Registered arenas: no CPU byte copies.  Per chunk: descriptors up (pinned,
- * 40 B per value), the values into the packed device arena -- the DMA
+ * 48 B per value), the values into the packed device arena -- the DMA
  * engines copy runs of values that lie (nearly) back to back in the caller's
  * arena, the GPU gathers the rest from the mapped arena -- the routed
- * kernels, then the GPU writes each result's produced bytes into its slot of
- * the mapped output arena, and out_len / err come back with the descriptors.
- * Two slots on two streams, so one chunk's transfers overlap the other's
- * kernels.  Compress chunks hold at least twice the routing's batch
- * threshold (the parse's time has a per-launch floor). */
+ * kernels, then the results into the caller's output slots -- decoded values
+ * whose slots abut as DMA runs, streams by the GPU writing each one's
+ * produced bytes -- and out_len / err come back with the descriptors.
+ *
+ * Chunks rotate over NSLOT slots, each with its own stream, buffers and
+ * compress scratch, so chunk k+1's transfers run beside chunk k's kernels and
+ * several chunks' compress launches run side by side: the one-lane-per-value
+ * parse of a launch has a latency floor (~68 ms for 64 KiB values, DESIGN.md
+ * §4.1) that mostly idles the GPU, so two or three overlapped launches cost
+ * about one.  Compress batches of at least 192 MiB go in at least NSLOT
+ * chunks (LZF_GPU_HOST_CHUNK_MB caps a chunk, default 2048) through the
+ * routed generations whatever the chunk's count; decompress chunks hold
+ * 256 MiB of output. */
 void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *in_map, uint8_t *out_map)
 {
     make_slot_streams(c);
     /* per value: src_off, d_in_off, d_out_off, dst_off (u64), in_len, out_cap, out_len, err (u32) */
     const size_t mrec = 4 * sizeof(uint64_t) + 4 * sizeof(uint32_t);
-    uint64_t total_in = 0;
-    uint32_t max_len_all = 0;
-    for (uint32_t k = 0; k < v.count; k++) {
-        const uint32_t i = v.at(k);
-        total_in += a.compress ? a.in_len[i] : a.out_cap[i];
-        const uint32_t l = a.compress ? a.in_len[i] : a.out_cap[i];
-        if (l > max_len_all) max_len_all = l;
-    }
-    uint64_t chunk_bytes = 1024ull << 20;
-    if (const char *e = getenv("LZF_GPU_HOST_CHUNK_MB")) chunk_bytes = (uint64_t)strtoull(e, nullptr, 10) << 20;
-    if (chunk_bytes < (1u << 20)) chunk_bytes = 1u << 20;
-    uint32_t nchunks = (uint32_t)((total_in + chunk_bytes - 1) / chunk_bytes);
+    uint64_t total = 0;
+    for (uint32_t k = 0; k < v.count; k++) total += a.compress ? a.in_len[v.at(k)] : a.out_cap[v.at(k)];
+    uint32_t nchunks = 1;
+    bool bulk = false;
     if (a.compress) {
-        const uint32_t least = 2u * lzf_route_min_count(max_len_all);
-        const uint32_t most = least ? v.count / least : v.count;
-        if (nchunks > most) nchunks = most;
+        uint64_t chunk_bytes = 2048ull << 20;
+        if (const char *e = getenv("LZF_GPU_HOST_CHUNK_MB")) chunk_bytes = (uint64_t)strtoull(e, nullptr, 10) << 20;
+        if (chunk_bytes < (1u << 20)) chunk_bytes = 1u << 20;
+        if (total >= (192ull << 20) && v.count >= NSLOT * 1024u) {
+            nchunks = (uint32_t)((total + chunk_bytes - 1) / chunk_bytes);
+            if (nchunks < NSLOT) nchunks = NSLOT;
+            bulk = true;
+        }
+    } else {
+        nchunks = (uint32_t)((total + (256ull << 20) - 1) / (256ull << 20));
     }
+    if (nchunks > v.count) nchunks = v.count;
     if (nchunks < 1) nchunks = 1;
-    const uint32_t per_chunk = (v.count + nchunks - 1) / nchunks;
+    /* equal chunks (measured: compress chunks shrinking toward the end, so
+     * the last chunk's cand and scatter are short, were slower -- text64k
+     * 202 -> 211 ms, json4k 62 -> 66 -- its cand squeezes between running
+     * parses either way, and the parse's floor does not shrink with it) */
+    std::vector<uint32_t> bound;
+    for (uint32_t k = 0; k <= nchunks; k++) bound.push_back((uint32_t)((uint64_t)v.count * k / nchunks));
     const uint32_t min_len = a.compress ? 0u : 1u;
 
     auto drain = [&](Slot &sl) {
@@ -614,44 +637,55 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         }
         sl.busy = false;
     };
+    struct Run {
+        uint64_t host, dev, len;
+    };
+    std::vector<Run> iruns, oruns;
     uint32_t round = 0;
-    for (uint32_t k0 = 0; k0 < v.count; k0 += per_chunk, round++) {
-        const uint32_t n = v.count - k0 < per_chunk ? v.count - k0 : per_chunk;
-        Slot &sl = c.slot[round & 1u];
+    for (; round + 1 < bound.size(); round++) {
+        const uint32_t k0 = bound[round], n = bound[round + 1] - k0;
+        Slot &sl = c.slot[round % NSLOT];
         drain(sl);
         uint8_t *h_meta = (uint8_t *)sl.h_meta.get((size_t)n * mrec);
         uint64_t *m_src = (uint64_t *)h_meta, *m_din = m_src + n, *m_dout = m_din + n, *m_dst = m_dout + n;
         uint32_t *m_in_len = (uint32_t *)(m_dst + n), *m_cap = m_in_len + n;
-        /* device offsets keep each value's host address mod 16 (whole 16-byte
-         * moves); runs: consecutive values no more than 256 bytes apart in
-         * the caller's arena are copied as one DMA piece, gap bytes included
-         * (reads only, inside the registered range) */
-        struct Run {
-            uint64_t src, dst, len;
-        };
-        std::vector<Run> runs;
+        /* Device offsets keep each value's host address mod 16 (whole 16-byte
+         * moves).  Input runs: consecutive values at most 256 bytes apart in
+         * the caller's arena are one DMA piece, gap bytes included (reads
+         * only, inside the registered range).  Output runs (decode only):
+         * slots that abut exactly, so a DMA piece writes only the call's own
+         * slots. */
+        iruns.clear();
+        oruns.clear();
         uint64_t x = 0, y = 0;
         uint32_t max_len = 0;
         for (uint32_t k = 0; k < n; k++) {
             const uint32_t i = v.at(k0 + k);
             const uint64_t so = a.in_off[i], ext = in_extent(a, i);
-            if (!runs.empty() && so >= runs.back().src + runs.back().len && so - (runs.back().src + runs.back().len) <= 256u) {
-                Run &r = runs.back();
-                m_din[k] = r.dst + (so - r.src);
-                r.len = so + ext - r.src;
+            if (!iruns.empty() && so >= iruns.back().host + iruns.back().len &&
+                so - (iruns.back().host + iruns.back().len) <= 256u) {
+                Run &r = iruns.back();
+                m_din[k] = r.dev + (so - r.host);
+                if (so + ext - r.host > r.len) r.len = so + ext - r.host;
             } else {
-                const uint64_t ph = ((uintptr_t)in_map + so) & 15u;
-                x = ((x + 15u) & ~15ull) + ph;
-                runs.push_back(Run{so, x, ext});
+                x = ((x + 15u) & ~15ull) + (((uintptr_t)in_map + so) & 15u);
+                iruns.push_back(Run{so, x, ext});
                 m_din[k] = x;
             }
-            x = m_din[k] + ext;
-            const uint64_t oph = ((uintptr_t)out_map + a.out_off[i]) & 15u;
-            y = ((y + 15u) & ~15ull) + oph;
-            m_dout[k] = y;
-            y += a.out_cap[i];
+            if (m_din[k] + ext > x) x = m_din[k] + ext;
+            const uint64_t oo = a.out_off[i];
+            if (!a.compress && !oruns.empty() && oo == oruns.back().host + oruns.back().len) {
+                Run &r = oruns.back();
+                m_dout[k] = r.dev + r.len;
+                r.len += a.out_cap[i];
+            } else {
+                y = ((y + 15u) & ~15ull) + (((uintptr_t)out_map + oo) & 15u);
+                oruns.push_back(Run{oo, y, a.out_cap[i]});
+                m_dout[k] = y;
+            }
+            y = m_dout[k] + a.out_cap[i];
             m_src[k] = so;
-            m_dst[k] = a.out_off[i];
+            m_dst[k] = oo;
             m_in_len[k] = a.in_len[i];
             m_cap[k] = a.out_cap[i];
             const uint32_t l = a.compress ? a.in_len[i] : a.out_cap[i];
@@ -666,14 +700,20 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
                        *d_dst = d_dout + n;
         const uint32_t *d_in_len = (const uint32_t *)(d_dst + n), *d_cap = d_in_len + n;
         uint32_t *d_out_len = (uint32_t *)(d_cap + n);
-        if (runs.size() <= 8u + n / 64u) {
-            for (const Run &r : runs)
+        const size_t few = 8u + n / 64u;
+        /* the chunks' inputs cross the bus one chunk after the other (side by
+         * side they would share the link and all arrive at the end): chunk
+         * k's kernels then start when its own inputs are in */
+        if (round) check(hipStreamWaitEvent(sl.stream, c.slot[(round - 1) % NSLOT].in_done, 0), "hipStreamWaitEvent");
+        if (iruns.size() <= few) {
+            for (const Run &r : iruns)
                 if (r.len)
-                    check(hipMemcpyAsync(d_in + r.dst, a.in + r.src, r.len, hipMemcpyHostToDevice, sl.stream),
+                    check(hipMemcpyAsync(d_in + r.dev, a.in + r.host, r.len, hipMemcpyHostToDevice, sl.stream),
                           "hipMemcpyAsync");
         } else {
             check(lzf_launch_move(in_map, d_src, d_in, d_din, d_in_len, min_len, n, sl.stream), "gather launch");
         }
+        check(hipEventRecord(sl.in_done, sl.stream), "hipEventRecord");
         LzfBatch b{};
         b.in = d_in;
         b.in_off = d_din;
@@ -685,8 +725,15 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         b.err = (int32_t *)(d_out_len + n);
         b.count = n;
         b.max_len = max_len;
-        check(launch(a, b, sl.stream), "kernel launch");
-        check(lzf_launch_move(d_out, d_dout, out_map, d_dst, d_out_len, 0u, n, sl.stream), "scatter launch");
+        check(bulk ? lzf_route_compress_bulk(b, sl.stream, sl.scratch) : launch(a, b, sl.stream), "kernel launch");
+        if (!a.compress && oruns.size() <= few) {
+            for (const Run &r : oruns)
+                if (r.len)
+                    check(hipMemcpyAsync(a.out + r.host, d_out + r.dev, r.len, hipMemcpyDeviceToHost, sl.stream),
+                          "hipMemcpyAsync");
+        } else {
+            check(lzf_launch_move(d_out, d_dout, out_map, d_dst, d_out_len, 0u, n, sl.stream), "scatter launch");
+        }
         check(hipMemcpyAsync(h_meta + res_off, d_meta + res_off, (size_t)n * mrec - res_off, hipMemcpyDeviceToHost,
                              sl.stream),
               "hipMemcpyAsync");
@@ -695,8 +742,7 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         sl.count = n;
         sl.busy = true;
     }
-    drain(c.slot[round & 1u]);
-    drain(c.slot[(round + 1u) & 1u]);
+    for (uint32_t k = 0; k < NSLOT; k++) drain(c.slot[(round + k) % NSLOT]);
 }
 
 /* the [lo, hi) byte ranges a sub-batch reads and writes in the caller's arenas */

@@ -114,6 +114,12 @@ hipError_t lzf_route_decompress(const LzfBatch &b, hipStream_t s);
 uint32_t lzf_route_min_count(uint32_t max_len);
 bool lzf_device_ok(int dev);
 void lzf_scratch_release_all(void);
+/* compress with the routed generations whatever the batch size, on a private
+ * scratch (lzf_scratch_create): the host pipeline's side-by-side chunks */
+hipError_t lzf_route_compress_bulk(const LzfBatch &b, hipStream_t s, void *scratch);
+void *lzf_scratch_create(void);
+void lzf_scratch_release(void *scratch);
+void lzf_scratch_destroy(void *scratch);
 const char *lzf_decompress_kernel_name(void);
 
 #endif

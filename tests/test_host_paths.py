@@ -108,6 +108,16 @@ def test_registered_contiguous_runs_and_exact_writes(oracle, registered):
         else:
             assert bytes(s[:olen[i]]) == exp, i
             assert (s[olen[i]:] == 0xA5).all(), i
+    # decoded values into abutting slots: the DMA engines write whole runs
+    ok = olen > 0
+    dec = registered(_aligned(count * n))
+    dl = np.zeros(int(ok.sum()), np.uint32)
+    er = np.zeros(int(ok.sum()), np.int32)
+    m = int(ok.sum())
+    gibson_amd.host_decompress_batch(out, oof[ok], olen[ok], dec, np.arange(m, dtype=np.uint64) * n,
+                                     np.full(m, n, np.uint32), dl, er)
+    assert (dl == n).all() and (er == 0).all()
+    assert np.array_equal(dec[:m * n].reshape(m, n), arena.reshape(count, n)[ok])
 
 
 def test_registered_decode_errors_and_empty_streams(oracle, registered):
@@ -188,3 +198,21 @@ def test_two_contexts_on_one_device_bit_exact(digests_full):
 def digests_full():
     with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
         return {(d["kind"], d["seed"], d["n"], d["count"]): d["sha256"] for d in json.load(f)["digests"]}
+
+
+def test_registered_bulk_chunks_config1_digest(digests_full, registered):
+    # 1 GiB of configs[1] through registered arenas: three side-by-side
+    # chunks on the slots' own scratch (the bulk route), bit-exact by the
+    # reference's digest of the first 262 144 values
+    import gibson_amd
+    from tests.digest import batch_digest
+    from tests.oracle_lib import _SYN
+    kind, seed, n, count = 1, 0x5EED0002, 4096, 262144
+    arena = registered(_aligned(count * n))
+    _SYN.synth_fill(kind, seed, 0, count, n, arena.ctypes.data)
+    off = np.arange(count, dtype=np.uint64) * n
+    out = registered(_aligned(count * n))
+    olen = np.zeros(count, np.uint32)
+    gibson_amd.host_compress_batch(arena, off, np.full(count, n, np.uint32), out, off,
+                                   np.full(count, n - 4, np.uint32), olen)
+    assert batch_digest(out, n, olen) == digests_full[(kind, seed, n, count)]

@@ -4,7 +4,12 @@ starts in the client buffer and ends in the trie-resident value).  Times
 lzf_host_compress_batch / lzf_host_decompress_batch on host arrays: staging
 into pinned memory, hipMemcpyAsync H2D, kernels, D2H, copy-out -- for
 DESIGN.md, never bench.py's `value`.
-usage: host_path_bench.py [KIND N COUNT REPS]"""
+usage: host_path_bench.py [KIND N COUNT REPS] [--register] [--devices LIST]
+  --register  lzf_host_register the three arenas first (the GPU moves the
+              values; no CPU packing)
+  --devices   LZF_GPU_DEVICES for this process (e.g. 0,0 or all): value i to
+              plan entry i mod G; the line reports each entry's spread"""
+import argparse
 import ctypes
 import json
 import os
@@ -12,38 +17,59 @@ import sys
 import time
 
 import numpy as np
-import torch  # noqa: F401  (before the library: one HIP runtime in the process)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-import gibson_amd  # noqa: E402
+
+
+def aligned(nbytes):
+    raw = np.zeros(nbytes + 8192, np.uint8)
+    k = (-raw.ctypes.data) % 4096
+    return raw[k:k + nbytes]
 
 
 def main():
-    kind, n, count, reps = (int(x, 0) for x in (sys.argv[1:5] if len(sys.argv) > 4
-                                                 else ("1", "4096", "65536", "5")))
+    ap = argparse.ArgumentParser()
+    ap.add_argument("pos", nargs="*", default=["1", "4096", "65536", "5"])
+    ap.add_argument("--register", action="store_true")
+    ap.add_argument("--devices", default=None)
+    args = ap.parse_args()
+    if args.devices:
+        os.environ["LZF_GPU_DEVICES"] = args.devices      # read once, at the library's first host call
+    import torch  # noqa: F401  (before the library: one HIP runtime in the process)
+    import gibson_amd
+    kind, n, count, reps = (int(x, 0) for x in (args.pos if len(args.pos) > 3 else ("1", "4096", "65536", "5")))
     syn = ctypes.CDLL(os.path.join(ROOT, "gibson_amd", "libgibson_synth.so"))
     syn.synth_fill.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                ctypes.c_uint32, ctypes.c_void_p]
-    arena = np.zeros(count * n, np.uint8)
+    arena = aligned(count * n)
     seed = {0: 0x5EED0004, 1: 0x5EED0002, 2: 0x5EED0003, 3: 0x5EED0005}.get(kind, 0x5EED0002)
     syn.synth_fill(kind, seed, 0, count, n, arena.ctypes.data)
     off = np.arange(count, dtype=np.uint64) * n
     ln = np.full(count, n, np.uint32)
     cap = np.full(count, n - 4, np.uint32)
-    out = np.zeros_like(arena)
+    out = aligned(count * n)
     olen = np.zeros(count, np.uint32)
-    dec = np.zeros_like(arena)
+    dec = aligned(count * n)
     dlen = np.zeros(count, np.uint32)
     err = np.zeros(count, np.int32)
+    reg_s = None
+    if args.register:
+        t0 = time.perf_counter()
+        for a in (arena, out, dec):
+            gibson_amd.host_register(a)
+        reg_s = time.perf_counter() - t0
     tc, td = [], []
+    spread_c = spread_d = None
     for r in range(reps + 1):
         t0 = time.perf_counter()
         gibson_amd.host_compress_batch(arena, off, ln, out, off, cap, olen)
         t1 = time.perf_counter()
+        spread_c = gibson_amd.host_last_spread()
         ok = olen > 0
         gibson_amd.host_decompress_batch(out, off[ok], olen[ok], dec, off[ok], ln[ok], dlen, err)
         t2 = time.perf_counter()
+        spread_d = gibson_amd.host_last_spread()
         if r:
             tc.append(t1 - t0)
             td.append(t2 - t1)
@@ -58,7 +84,15 @@ def main():
     # (bytes each part moves at its own measured rate)
     sum_c = count * n / parts["h2d_GBps"] + parts["compress_kernel_s"] * 1e9 + cb / parts["d2h_GBps"]
     sum_d = cb / parts["h2d_GBps"] + parts["decompress_kernel_s"] * 1e9 + count * n / parts["d2h_GBps"]
-    print(json.dumps({"path": "host memory -> pinned staging -> H2D -> kernel -> D2H -> host",
+    path = ("registered host arenas -> GPU gather / DMA runs -> kernel -> GPU scatter -> host" if args.register
+            else "host memory -> pinned staging -> H2D -> kernel -> D2H -> host")
+    plan = gibson_amd.device_plan()
+    if args.register:
+        for a in (arena, out, dec):
+            gibson_amd.host_unregister(a)
+    print(json.dumps({"path": path, "devices": plan, "register_s": reg_s,
+                      "spread_last_rep": {"compress": [[v, round(ms, 2)] for v, ms in spread_c],
+                                          "decompress": [[v, round(ms, 2)] for v, ms in spread_d]},
                       "kind": kind, "seed": hex(seed), "n": n, "count": count, "in_bytes": count * n,
                       "compress_GBps": round(count * n / c / 1e9, 3),
                       "decompress_GBps": round(count * n / d / 1e9, 3),
@@ -74,7 +108,8 @@ def parts_of(arena, out, olen, n, count):
     """the path's parts measured alone: pinned H2D and D2H of the arena, and
     the device-resident kernels on the same values"""
     import torch
-    hp = torch.from_numpy(arena).pin_memory()
+    import gibson_amd
+    hp = torch.from_numpy(np.ascontiguousarray(arena)).pin_memory()
     dv = torch.empty(count * n, dtype=torch.uint8, device="cuda")
     t = []
     for r in range(4):
