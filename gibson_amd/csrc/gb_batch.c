@@ -239,41 +239,48 @@ long gb_mget_payload(const uint8_t *keys, const uint64_t *key_off, const uint32_
             int32_t *se = malloc(ns * sizeof *se);
             uint64_t *so = malloc(ns * sizeof *so);
             uint32_t *sl = malloc(ns * sizeof *sl), *sk = malloc(ns * sizeof *sk);
-            for (uint32_t k = 0, j = 0; sk && k < m; k++) {
+            /* any failure here fails the call (ret), as the first pass does:
+             * the reply is never built from a half-failed retry */
+            int rc2 = se && so && sl && sk ? LZF_GPU_OK : LZF_GPU_ENOMEM;
+            for (uint32_t k = 0, j = 0; rc2 == LZF_GPU_OK && k < m; k++) {
                 if (dl[k] || exact[k]) continue;
                 uo[j] = ioff[k];
                 ul[j] = len[k];
                 sk[j++] = k;
             }
-            int ok = se && so && sl && sk &&
-                     lzf_host_decoded_size_batch(vals, uo, ul, us, se, ns, maxrequestsize) == LZF_GPU_OK;
+            if (rc2 == LZF_GPU_OK) rc2 = lzf_host_decoded_size_batch(vals, uo, ul, us, se, ns, maxrequestsize);
             uint64_t add = 0;
-            for (uint32_t j = 0; ok && j < ns; j++) {
+            for (uint32_t j = 0; rc2 == LZF_GPU_OK && j < ns; j++) {
                 so[j] = total + add;
                 add += us[j];
             }
-            uint8_t *b = ok && add ? realloc(dec, total + add) : NULL;
-            if (ok && add && !b) {
+            if (rc2 == LZF_GPU_OK && add) {
+                uint8_t *b = realloc(dec, total + add);
+                if (!b) {
+                    rc2 = LZF_GPU_ENOMEM;
+                } else {
+                    dec = b;
+                    /* items that do not decode at all keep size 0 (us == 0) */
+                    rc2 = lzf_host_decompress_batch(vals, uo, ul, dec, so, us, sl, se, ns);
+                    if (rc2 == LZF_GPU_OK) {
+                        for (uint32_t j = 0; j < ns; j++) {
+                            if (!us[j] || !sl[j]) continue;
+                            dl[sk[j]] = sl[j];
+                            er[sk[j]] = 0;
+                            ooff[sk[j]] = so[j];
+                        }
+                        total += add;
+                        g_mget_staged = total;
+                    }
+                }
+            }
+            if (rc2 != LZF_GPU_OK) {
                 free(se);
                 free(so);
                 free(sl);
                 free(sk);
-                ret = LZF_GPU_ENOMEM;
+                ret = rc2;
                 goto done;
-            }
-            if (b) {
-                dec = b;
-                /* items that do not decode at all keep size 0 (us == 0) */
-                if (lzf_host_decompress_batch(vals, uo, ul, dec, so, us, sl, se, ns) == LZF_GPU_OK) {
-                    for (uint32_t j = 0; j < ns; j++) {
-                        if (!us[j] || !sl[j]) continue;
-                        dl[sk[j]] = sl[j];
-                        er[sk[j]] = 0;
-                        ooff[sk[j]] = so[j];
-                    }
-                    total += add;
-                    g_mget_staged = total;
-                }
             }
             free(se);
             free(so);

@@ -16,6 +16,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -94,6 +96,12 @@ bool device_ok(int dev)
  * runs lzf_gpu_selfcheck() first, outside the capture. */
 int g_order[64];                     /* 0 unchecked, 1 held, -1 violated */
 int g_order_last[64];                /* the last probe's outcome, -2: it could not run */
+/* a probe that could not run is retried no sooner than this (a backoff
+ * doubling from 100 ms to 10 s, so a lasting failure -- memory pressure, a
+ * caller capturing a graph -- does not cost every compress call a probe
+ * under the mutex) */
+std::chrono::steady_clock::time_point g_order_retry[64];
+std::chrono::milliseconds g_order_backoff[64];
 std::mutex g_order_mu;
 
 int lds_order_state(bool run)
@@ -101,11 +109,18 @@ int lds_order_state(bool run)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -2;
     std::lock_guard<std::mutex> lk(g_order_mu);
-    if (!g_order[dev] && run) {
+    const auto now = std::chrono::steady_clock::now();
+    if (!g_order[dev] && run && (g_order_last[dev] != -2 || now >= g_order_retry[dev])) {
         const char *f = getenv("LZF_GPU_FORCE_ORDER_FAIL");
         const int bad = (f && *f == '1') ? 1 : lzf_lds_order_check(dev);
         g_order_last[dev] = bad == 0 ? 1 : bad > 0 ? -1 : -2;
-        if (bad >= 0) g_order[dev] = g_order_last[dev];
+        if (bad >= 0) {
+            g_order[dev] = g_order_last[dev];
+        } else {
+            auto &b = g_order_backoff[dev];
+            b = b.count() ? std::min(b * 2, std::chrono::milliseconds(10000)) : std::chrono::milliseconds(100);
+            g_order_retry[dev] = now + b;
+        }
         return g_order_last[dev];
     }
     return g_order[dev] ? g_order[dev] : g_order_last[dev];

@@ -447,122 +447,18 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
  * (16-byte aligned), so it overwrites only bytes before
  * base_{k+1} + 320 - 512 <= base_k - 32 (base_{k+1} <= base_k + 160) */
 #define CD_IN_RINGP 512u
-/* CD_TOKOUT: the input ring's first 32 bytes are mirrored right after it
- * (also tried for single unaligned reads of a token's bytes in steps 1-2:
- * slower, 11.14 -> 11.85 ms mixed16k, 21.75 -> 24.00 Zipf, 17.33 -> 18.88
- * text64k, profiles/r04/dab_*_noper_nomir.txt) */
-#define CD_IN_MIRROR 32u
-#ifndef CD_TOKOUT
-#define CD_TOKOUT 0
-#endif
-/* LDS store of exactly m (1..16) bytes of v at p (unaligned: gfx950's LDS
- * takes unaligned b128/b64/b32/b16 accesses) */
-__device__ __forceinline__ void cd_st(uint8_t *p, uint4 v, uint32_t m)
-{
-    if (m >= 16u) {
-        __builtin_memcpy(p, &v, 16);
-        return;
-    }
-    uint32_t a = v.x, b = v.y, c = v.z, d = v.w;
-    if (m & 8u) {
-        const uint2 t = make_uint2(a, b);
-        __builtin_memcpy(p, &t, 8);
-        p += 8;
-        a = c;
-        b = d;
-    }
-    if (m & 4u) {
-        __builtin_memcpy(p, &a, 4);
-        p += 4;
-        a = b;
-    }
-    if (m & 2u) {
-        const uint16_t t = (uint16_t)a;
-        __builtin_memcpy(p, &t, 2);
-        p += 2;
-        a >>= 16;
-    }
-    if (m & 1u) *p = (uint8_t)a;
-}
+/* Round 4 measured and removed: a token-granular output stage (one lane
+ * per token, 16-byte unaligned LDS copies, a pass per in-round reference
+ * chain: Zipf 1 M x 8 KiB 20.27 -> 102.30 ms, DESIGN.md §4.4,
+ * profiles/r04/dab_*_tok.txt), and the input ring's first 32 bytes mirrored
+ * past its end for single unaligned token reads in steps 1-2 (slower:
+ * 11.14 -> 11.85 ms mixed16k, 21.75 -> 24.00 Zipf, 17.33 -> 18.88 text64k,
+ * profiles/r04/dab_*_noper_nomir.txt). */
 
-__device__ __forceinline__ uint4 cd_ld(const uint8_t *p)
-{
-    uint4 v;
-    __builtin_memcpy(&v, p, 16);
-    return v;
-}
-
-/* Token-granular output of one round (CD_TOKOUT, rounds whose output stays
- * inside the window: O + total <= ring, so positions are ring offsets and
- * nothing wraps or is overwritten).  Lane l copies token l whole, 16 bytes
- * per LDS access (src/lzf_d.c:86-91 literal, :133-142 back-reference):
- *   - a literal from the input ring (its first 32 bytes are mirrored past
- *     its end, so a token's bytes are contiguous);
- *   - a back-reference from the window, 16 bytes at a time; one that overlaps
- *     itself (distance d < 16 and d < length: the byte-serial copy replicates
- *     the last d bytes) first writes one period multiple L = d * ceil(16 / d)
- *     byte by byte, then copies 16 bytes at a time from L back.
- * A token is copied in the first pass in which no token before it that is
- * still pending can overlap its source: the nearest pending token before it
- * ends at or before its source, or its source lies wholly before the round.
- * The lowest pending token always qualifies, so every pass makes progress;
- * passes follow the round's in-round reference chains. */
-__device__ __forceinline__ void cd_output_tok(uint8_t *inr, uint8_t *outr, uint8_t *dst, uint32_t O, uint32_t total,
-                                              uint32_t ntok, uint32_t w, uint32_t lane, uint32_t unit, uint32_t &F)
-{
-    const bool act = lane < ntok;
-    const uint32_t rel = w & 0xFFFFu, info = w >> 17;
-    const bool lit = (w >> 16) & 1u;
-    const uint32_t nrel = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane + 1u) & 63u) << 2), (int)rel);
-    const uint32_t len = act ? ((lane + 1u < ntok ? nrel : total) - rel) : 0u;
-    const uint32_t Ot = O + rel, end = Ot + len;
-    /* a back-reference's source [s, e): the bytes it reads that precede it */
-    const uint32_t s = lit ? 0u : Ot - info;
-    const uint32_t e = lit ? 0u : (s + len < Ot ? s + len : Ot);
-    bool done = !act;
-    for (;;) {
-        const uint64_t D = cd_ballot(done);
-        if (D == ~0ull) break;
-        const uint64_t before = ~D & ((1ull << lane) - 1ull);
-        const uint32_t js = before ? 63u - (uint32_t)__builtin_clzll(before) : 0u;
-        const uint32_t endj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(js << 2), (int)end);
-        const bool ready = !done && (lit || e <= O || before == 0ull || endj <= s);
-        if (ready) {
-            if (lit) {
-                const uint32_t ri = (Ot - info) & (CD_IN_RINGP - 1u);
-                for (uint32_t c = 0; c < len; c += 16u)
-                    cd_st(outr + Ot + c, cd_ld(inr + ri + c), len - c);
-            } else {
-                uint32_t d = info, c = 0u;
-                if (d < 16u && d < len) {
-                    const uint32_t L = d * ((15u + d) / d);
-                    const uint32_t pre = len < L ? len : L;
-                    for (; c < pre; c++) outr[Ot + c] = outr[Ot + c - d];
-                    d = L;
-                }
-                for (; c < len; c += 16u) cd_st(outr + Ot + c, cd_ld(outr + Ot + c - d), len - c);
-            }
-        }
-        cd_fence();
-        done = done || ready;
-#ifdef CD_TIMING
-        if (lane == 0u) atomicAdd(&cd_tstat[4], 1ull);      /* passes */
-#endif
-    }
-#ifdef CD_TIMING
-    if (lane == 0u) {
-        atomicAdd(&cd_tstat[5], 1ull);                       /* rounds in token mode */
-        atomicAdd(&cd_tstat[6], (unsigned long long)ntok);   /* their tokens */
-    }
-#endif
-    /* completed flush units to HBM, 16 bytes per lane */
-    while (O + total - F >= unit) {
-        if (16u * lane < unit) __builtin_memcpy(dst + F + 16u * lane, outr + F + 16u * lane, 16);
-        F += unit;
-    }
-}
-
-/* a value past the batch's stated max_out_cap is refused, never overrun */
+/* a value past the batch's stated max_out_cap is refused, never overrun.
+ * The 16-bit start marks of tokpar64's windows of <= 4 KiB rely on this:
+ * with out_cap <= max_len <= the window, a stream's output positions stay
+ * below 65536, so a stale mark never matches a later group */
 __device__ __forceinline__ bool cd_refused(const LzfBatch &bt, uint32_t v, uint32_t lane)
 {
     if (bt.out_cap[v] <= bt.max_len) return false;
@@ -574,7 +470,8 @@ __device__ __forceinline__ bool cd_refused(const LzfBatch &bt, uint32_t v, uint3
 }
 
 /* CD_TP_SMALL: windows up to 4 KiB (the output stays below 65536, so 16-bit
- * start marks match only in their group) keep 16-bit marks and compute token
+ * start marks match only in their group: cd_refused holds out_cap to the
+ * batch's max_len, and lzf_launch_decompress picks no window below max_len) keep 16-bit marks and compute token
  * sizes instead of reading the 256-byte table: 5008 bytes of LDS for a 4 KiB
  * window, 32 streams per CU (the wave limit) instead of 30 */
 #ifndef CD_TP_SMALL
@@ -660,7 +557,6 @@ __device__ __forceinline__ void cd_stage_pipe(uint8_t *inr, const uint8_t *src, 
         if (x < to) {
             const uint4 v = cd_ld16(src + x, to - x);
             *(uint4 *)(inr + (x & (CD_IN_RINGP - 1u))) = v;
-            if (CD_TOKOUT && (x & (CD_IN_RINGP - 1u)) < CD_IN_MIRROR) *(uint4 *)(inr + CD_IN_RINGP + (x & (CD_IN_RINGP - 1u))) = v;
         }
         loaded = to;
         cd_fence();
@@ -671,7 +567,7 @@ __device__ __forceinline__ void cd_stage_pipe(uint8_t *inr, const uint8_t *src, 
  * static: the compiler folds the LDS base into every address (with dynamic
  * LDS it adds the base, 0, with one VALU per LDS address) */
 #define CD_PIPE_LDS (CD_IN_RINGP + 2u * sizeof(CdSlot) + 5u * CD_LANES + 16u + CD_OUT_MAX + \
-                     (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u) + 512u)   /* + jump and token-size tables */
+                     512u)   /* + jump and token-size tables */
 __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, uint32_t out_ring)
 {
     __shared__ __attribute__((aligned(16))) uint8_t smem[CD_PIPE_LDS];
@@ -680,9 +576,8 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
     uint32_t *mark = (uint32_t *)(slot + 2);           /* the consumer's 64 token-start marks */
     uint8_t *mark64 = (uint8_t *)(mark + CD_LANES);    /* mark slot 64 (write-only) and spare */
     uint8_t *outr = mark64 + CD_LANES;                 /* out_ring (power of two) */
-    uint8_t *inr = outr + out_ring;                    /* CD_IN_RINGP, right after the window (cd_output);
-                                                          CD_TOKOUT: + the mirror and 16 bytes */
-    uint8_t *jt = inr + CD_IN_RINGP + (CD_TOKOUT ? CD_IN_MIRROR + 16u : 0u);   /* the jump table (+ token sizes) */
+    uint8_t *inr = outr + out_ring;                    /* CD_IN_RINGP, right after the window (cd_output) */
+    uint8_t *jt = inr + CD_IN_RINGP;                   /* the jump table (+ token sizes) */
     uint8_t *sink = jt + 512u;                         /* the consumer's idle-lane byte sink, past the window */
     const uint32_t imask = CD_IN_RINGP - 1u, omask = out_ring - 1u;
 
@@ -716,8 +611,6 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
                 const uint32_t px = loaded + 16u * lane;
                 if (px < pto) {
                     *(uint4 *)(inr + (px & (CD_IN_RINGP - 1u))) = pv;
-                    if (CD_TOKOUT && (px & (CD_IN_RINGP - 1u)) < CD_IN_MIRROR)
-                        *(uint4 *)(inr + CD_IN_RINGP + (px & (CD_IN_RINGP - 1u))) = pv;
                 }
                 loaded = pto;
                 pend = false;
@@ -770,10 +663,7 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
             err = __builtin_amdgcn_readfirstlane(s.err);
             if (err) break;      /* the failing round writes nothing */
             const uint32_t w = s.tok[lane];
-            if (CD_TOKOUT && O + total <= omask + 1u)
-                cd_output_tok(inr, outr, dst, O, total, ntok, w, lane,
-                              (omask + 1u) / 2u < 1024u ? (omask + 1u) / 2u : 1024u, F);
-            else if (CD_PERIOD && per)   /* its own copy of the loop: the other rounds run the plain one */
+            if (CD_PERIOD && per)   /* its own copy of the loop: the other rounds run the plain one */
                 cd_output<CD_IN_RINGP, true, CD_MARKAHEAD_PIPE>(smem, (uint32_t)(outr - smem), omask, mark, (uint32_t)(sink - smem), dst,
                                              O, total, lane < ntok, O + (w & 0xFFFFu),
                                              (w >> 17) | ((w & 0x10000u) << 15), lane, F);
@@ -817,7 +707,10 @@ hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s)
         if (ring != CD_OUT_MAX) return hipErrorInvalidValue;   /* static LDS for the 8 KiB window */
         hipLaunchKernelGGL(lzf_decompress_pipe_kernel, dim3(b.count), dim3(2u * CD_LANES), 0, s, b, ring);
     } else {
-        /* LDS: the input ring, the window, the 64 marks and token starts */
+        /* LDS: the input ring, the window, the 64 marks and token starts.
+         * A window of <= 4 KiB covers max_len (its 16-bit marks need every
+         * output below 65536, CD_TP_SMALL); the 8 KiB one is a ring */
+        if (ring <= 4096u && b.max_len > ring) return hipErrorInvalidValue;
         switch (ring) {
         case 256u: hipLaunchKernelGGL(lzf_decompress_tokpar_kernel<256u>, dim3(b.count), dim3(CD_LANES), 0, s, b, ring); break;
         case 512u: hipLaunchKernelGGL(lzf_decompress_tokpar_kernel<512u>, dim3(b.count), dim3(CD_LANES), 0, s, b, ring); break;

@@ -39,3 +39,36 @@ int ref_batch_compress(int kind, uint64_t seed, uint64_t first, uint32_t count, 
     }
     return bad ? -1 : 0;
 }
+
+unsigned int ref_lzf_decompress(const void *, unsigned int, void *, unsigned int);
+
+/* the reference round trip of values first .. first+count-1: value k's
+ * stream (out_len n - out_slack) at out + k*n with its length in lens[k],
+ * then -- for the values that fit -- the reference decoder's output at
+ * dec + k*n (out_len n) with its length in dlens[k] (0 for values that did
+ * not compress); the decode-only digests of BASELINE configs[3] */
+int ref_batch_roundtrip(int kind, uint64_t seed, uint64_t first, uint32_t count, uint32_t n,
+                        uint32_t out_slack, uint8_t *out, uint32_t *lens, uint8_t *dec, uint32_t *dlens,
+                        int threads)
+{
+    if (threads > 0) omp_set_num_threads(threads);
+    int bad = 0;
+#pragma omp parallel
+    {
+        uint8_t *buf = (uint8_t *)__builtin_malloc(n + 16);
+        if (!buf) {
+#pragma omp atomic write
+            bad = 1;
+        } else {
+#pragma omp for schedule(static)
+            for (uint32_t k = 0; k < count; k++) {
+                syn_generate(kind, seed, first + k, buf, n);
+                uint8_t *o = out + (uint64_t)k * n;
+                lens[k] = ref_lzf_compress(buf, n, o, n - out_slack);
+                dlens[k] = lens[k] ? ref_lzf_decompress(o, lens[k], dec + (uint64_t)k * n, n) : 0u;
+            }
+            __builtin_free(buf);
+        }
+    }
+    return bad ? -1 : 0;
+}

@@ -164,42 +164,75 @@ DIGEST_CONFIGS = [
     (2, 2, 0x5EED0003, 65536, 262144),
     (3, 0, 0x5EED0004, 8192, 65536),
     (4, 3, 0x5EED0005, 16384, 65536),
-    # the production routes at their real batch sizes (at least
-    # lzf_api.cpp lane_min_count values: 163 840 of <= 4 KiB, 81 920 of
-    # <= 16 KiB): both take the lane generation, the stream cand kernel
+    # the production routes at their real batch sizes (above
+    # gibson_amd/csrc/lzf_api.cpp lane_min_count, the routing's batch
+    # thresholds): both take the lane generation, the stream cand kernel
     # (lzf_stream.hip) and the lane parse
     (1, 1, 0x5EED0002, 4096, 262144),
     (4, 3, 0x5EED0005, 16384, 131072),
+    # round 5: the configs' real counts -- all of configs[1], the first
+    # 1 M-value chunk of configs[4] (the chunk bench.py runs), and 1 M values
+    # of configs[3] with the reference decoder's output digest (ROUNDTRIP)
+    (1, 1, 0x5EED0002, 4096, 1048576),
+    (4, 3, 0x5EED0005, 16384, 1048576),
+    (3, 0, 0x5EED0004, 8192, 1048576),
 ]
+# configs whose record also holds decoded_sha256: sha256 over the values in
+# order of (u32 LE decoded length || the reference decoder's output), the
+# length 0 for a value that did not compress
+ROUNDTRIP = {(0, 0x5EED0004, 8192, 1048576)}
 
 
-def digests():
+def digests(have=()):
+    """reference digests of DIGEST_CONFIGS, skipping the (kind, seed, n,
+    count) keys in ``have``"""
     import numpy as np
     lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libref_batch.so"))
     lib.ref_batch_compress.restype = ctypes.c_int
     lib.ref_batch_compress.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                        ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_int]
+    lib.ref_batch_roundtrip.restype = ctypes.c_int
+    lib.ref_batch_roundtrip.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                        ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     res = []
     for cfg, kind, seed, n, count in DIGEST_CONFIGS:
-        h = hashlib.sha256()
+        if (kind, seed, n, count) in have:
+            continue
+        rt = (kind, seed, n, count) in ROUNDTRIP
+        h, hd = hashlib.sha256(), hashlib.sha256()
         chunk = max(1, min(count, (512 << 20) // n))
         out = np.empty(chunk * n, np.uint8)
         lens = np.empty(chunk, np.uint32)
+        dec = np.empty(chunk * n, np.uint8) if rt else None
+        dlens = np.empty(chunk, np.uint32) if rt else None
         total = comp = 0
         for first in range(0, count, chunk):
             m = min(chunk, count - first)
-            rc = lib.ref_batch_compress(kind, seed, first, m, n, 4, out.ctypes.data, lens.ctypes.data,
-                                        os.cpu_count() or 1)
+            if rt:
+                rc = lib.ref_batch_roundtrip(kind, seed, first, m, n, 4, out.ctypes.data, lens.ctypes.data,
+                                             dec.ctypes.data, dlens.ctypes.data, os.cpu_count() or 1)
+            else:
+                rc = lib.ref_batch_compress(kind, seed, first, m, n, 4, out.ctypes.data, lens.ctypes.data,
+                                            os.cpu_count() or 1)
             assert rc == 0
             for k in range(m):
                 ln = int(lens[k])
                 h.update(ln.to_bytes(4, "little"))
-                h.update(out[k * n:k * n + ln].tobytes())
+                h.update(out[k * n:k * n + ln].data)
                 comp += ln
+                if rt:
+                    dl = int(dlens[k])
+                    hd.update(dl.to_bytes(4, "little"))
+                    hd.update(dec[k * n:k * n + dl].data)
             total += m
-        res.append({"config": cfg, "kind": kind, "seed": seed, "n": n, "first": 0, "count": count,
-                    "out_len": "n-4", "sha256": h.hexdigest(), "comp_bytes": comp})
+        rec = {"config": cfg, "kind": kind, "seed": seed, "n": n, "first": 0, "count": count,
+               "out_len": "n-4", "sha256": h.hexdigest(), "comp_bytes": comp}
+        if rt:
+            rec["decoded_sha256"] = hd.hexdigest()
+            rec["decode_out_len"] = "n"
+        res.append(rec)
         print("digest", cfg, n, count, h.hexdigest()[:16], comp / (count * n))
     return res
 
@@ -229,6 +262,16 @@ def main():
             json.dump({"generator": "tests/golden/make_golden.py config0",
                        "source": "oracle/_ref/liblzf_ref.so (reference lzf_c.c, lzf_d.c)", **c0}, f, indent=1)
         print("config0", c0["stream_len"], c0["stream_sha256"][:16])
+        return 0
+    if len(sys.argv) > 1 and sys.argv[1] == "digests-add":
+        # append the DIGEST_CONFIGS records digests.json does not hold yet
+        path = os.path.join(here, "digests.json")
+        with open(path) as f:
+            doc = json.load(f)
+        have = {(d["kind"], d["seed"], d["n"], d["count"]) for d in doc["digests"]}
+        doc["digests"] += digests(have)
+        with open(path, "w") as f:
+            json.dump(doc, f, indent=1)
         return 0
     if len(sys.argv) > 1 and sys.argv[1] == "digests":
         with open(os.path.join(here, "digests.json"), "w") as f:

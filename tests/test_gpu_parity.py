@@ -578,6 +578,22 @@ def test_full_batch_digest_wtab(kind, seed, n, count, digests, monkeypatch, diag
     _digest_case(kind, seed, n, count, digests)
 
 
+# the configs' real counts (round 5): all 1 048 576 values of configs[1], the
+# first 1 M-value chunk of configs[4] (the chunk bench.py runs), and 1 M
+# values of configs[3] whose decoded output is also checked against the
+# reference decoder's (decoded_sha256)
+FULL = [(1, 0x5EED0002, 4096, 1048576), (3, 0x5EED0005, 16384, 1048576), (0, 0x5EED0004, 8192, 1048576)]
+
+
+@pytest.mark.parametrize("kind,seed,n,count", FULL)
+def test_full_count_digest(kind, seed, n, count, digests, monkeypatch):
+    import json
+    monkeypatch.delenv("LZF_GPU_LANE_MIN", raising=False)
+    with open(os.path.join(os.path.dirname(__file__), "golden", "digests.json")) as f:
+        rec = {(d["kind"], d["seed"], d["n"], d["count"]): d for d in json.load(f)["digests"]}
+    _digest_case(kind, seed, n, count, digests, decoded=rec[(kind, seed, n, count)].get("decoded_sha256"))
+
+
 def test_full_batch_digest_chunked_scratch(digests, monkeypatch):
     # configs[2]'s 262 144 x 64 KiB under a 16 GiB scratch cap: the table
     # generation in five chunks (a GPU-sharing server's route), bit-exact by
@@ -588,7 +604,7 @@ def test_full_batch_digest_chunked_scratch(digests, monkeypatch):
     assert _chunks() == 5, _chunks()
 
 
-def _digest_case(kind, seed, n, count, digests):
+def _digest_case(kind, seed, n, count, digests, decoded=None):
     import gibson_amd
     from tests.digest import batch_digest
     dev = "cuda"
@@ -612,6 +628,11 @@ def _digest_case(kind, seed, n, count, digests):
     gibson_amd.decompress_batch(comp, in_off, torch.where(ok, clen, torch.ones_like(clen)),
                                 dec, in_off, dcap, dlen, err, n)
     torch.cuda.synchronize()
+    if decoded is not None:
+        # the decoder's output, every value, against the reference decoder's
+        del comp
+        dl = torch.where(ok, dlen, torch.zeros_like(dlen)).cpu().numpy()
+        assert batch_digest(dec.cpu().numpy(), n, dl) == decoded
     assert torch.equal(dlen[ok], torch.full_like(dlen[ok], n))
     for r0 in range(0, count, 16384):
         r1 = min(count, r0 + 16384)
