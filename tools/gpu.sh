@@ -9,6 +9,7 @@
 #   tests[:EXPR]        the -m gpu suite (pytest -k EXPR)
 #   smoke               __graft_entry__.smoke()
 #   bench[:ARGS]        bench.py line (ARGS comma-separated, e.g. bench:--workload,json4k)
+#   benv:LABEL:ENV:ARGS bench.py ARGS under ENV (VAR=x,VAR2=y) -> bench_LABEL.json
 #   prof:LABEL:ARGS     rocprofv3 --kernel-trace --stats of bench.py ARGS -> kernel_stats_LABEL.txt
 #   pmc:LABEL:ARGS      FETCH_SIZE and WRITE_SIZE passes of bench.py ARGS (one counter per run)
 #   mix:LABEL:ARGS      instruction-mix counter sets of bench.py ARGS (one set per run) -> mix_LABEL.txt
@@ -46,6 +47,10 @@ for st in "$@"; do
       a=${st#bench}; a=${a#:}; a=${a//,/ }; lab=$(echo "main$a" | tr -c 'a-zA-Z0-9\n' '_')
       timeout -k 10 600 python bench.py $a > $O/bench_$lab.json 2> $O/bench_$lab.err || exit 1
       tail -1 $O/bench_$lab.json | cut -c1-900 ;;
+    benv:*)
+      IFS=: read -r _ lab envs args <<< "$st"; args=${args//,/ }; envs=${envs//,/ }
+      env $envs timeout -k 10 600 python bench.py $args > $O/bench_$lab.json 2> $O/bench_$lab.err || exit 1
+      tail -1 $O/bench_$lab.json | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["roofline"].get("per_kernel_ms"), d["config"].get("roundtrip_ok"))' ;;
     prof:*)
       IFS=: read -r _ lab args <<< "$st"; args=${args//,/ }
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_$lab -o run -- python3 bench.py $args --no-cpu > $O/prof_$lab.log 2>&1 || exit 1
