@@ -320,9 +320,27 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s, Scratch *own = null
         if ((!bulk && b.count < lane_min_count(b.max_len)) || !lzf_table_compress_supported(b.max_len))
             return lzf_launch_compress(b, s);
         /* the lane generation where its kernel 1 takes the batch (a
-         * diagnostic LZF_GPU_CAND=small stops at 4 KiB), else the table one */
-        return lane_compress(b, s, b.max_len <= LANE_DEFAULT_MAX && lzf_lane_compress_supported(b.max_len)
-                                       ? SU_LANE : SU_TABLE, own);
+         * diagnostic LZF_GPU_CAND=small stops at 4 KiB), else the table one --
+         * unless the scratch cap splits the table generation into more chunks
+         * than the lane generation (half the scratch per value): every chunk
+         * pays the parse's per-launch floor, so the chunk count decides
+         * (configs[2] under a 16 GiB cap: table 5 chunks 441 ms, lane 3 chunks
+         * 335 ms; 8 GiB: 712 / 488; uncapped table 190 vs lane 214,
+         * profiles/r05/cap/) */
+        {
+            bool lane = b.max_len <= LANE_DEFAULT_MAX && lzf_lane_compress_supported(b.max_len);
+            if (!lane && lzf_lane_compress_supported(b.max_len)) {
+                int dev = 0;
+                if (hipGetDevice(&dev) == hipSuccess) {
+                    const Scratch &S = own ? *own : g_scratch[dev & 63];
+                    const size_t lim = scratch_limit(S.cap);
+                    const uint64_t need_t = (uint64_t)b.count * lzf_table_scratch_per_value(b.max_len);
+                    const uint64_t need_l = (uint64_t)b.count * lzf_lane_scratch_per_value(b.max_len);
+                    lane = (need_t + lim - 1) / lim > (need_l + lim - 1) / lim;
+                }
+            }
+            return lane_compress(b, s, lane ? SU_LANE : SU_TABLE, own);
+        }
     }
 }
 

@@ -594,14 +594,18 @@ def test_full_count_digest(kind, seed, n, count, digests, monkeypatch):
     _digest_case(kind, seed, n, count, digests, decoded=rec[(kind, seed, n, count)].get("decoded_sha256"))
 
 
-def test_full_batch_digest_chunked_scratch(digests, monkeypatch):
-    # configs[2]'s 262 144 x 64 KiB under a 16 GiB scratch cap: the table
-    # generation in five chunks (a GPU-sharing server's route), bit-exact by
-    # the reference's digest
+@pytest.mark.parametrize("gen,chunks", [("default", 3), ("table", 5)])
+def test_full_batch_digest_chunked_scratch(digests, monkeypatch, gen, chunks):
+    # configs[2]'s 262 144 x 64 KiB under a 16 GiB scratch cap (a GPU-sharing
+    # server's route), bit-exact by the reference's digest: by default the
+    # lane generation, whose half-size scratch needs three chunks where the
+    # table generation (forced) needs five
     monkeypatch.delenv("LZF_GPU_LANE_MIN", raising=False)
     monkeypatch.setenv("LZF_GPU_SCRATCH_MB", "16384")
+    if gen == "table":
+        monkeypatch.setenv("LZF_GPU_KERNEL", "table")
     _digest_case(2, 0x5EED0003, 65536, 262144, digests)
-    assert _chunks() == 5, _chunks()
+    assert _chunks() == chunks, _chunks()
 
 
 def _digest_case(kind, seed, n, count, digests, decoded=None):
