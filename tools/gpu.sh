@@ -17,6 +17,7 @@
 #   dab:K:N:C:V[:V..]   the same for the decoder (AB_MODE=decompress)
 #   env:K:N:C:S[:S..]   compress A/B of env settings (tools/ab_env.py; a setting uses , and =)
 #   tstat:K:N:C         the pipe decoder's phase cycles (CD_TIMING build liblzf_hip_time.so)
+#   kt:K:N:C:LIB        per-phase cycles of the table cand kernel (-DKT_TIMING build liblzf_hip_LIB.so)
 #   xo:K:N:C:COUNTS     routed generation vs window64 by batch size (tools/crossover.py)
 #   host[:reg]          PCIe-inclusive host-path rates (tools/host_path_bench.py); :reg registered only
 #   trace:LABEL:ARGS    kernel + copy timeline of tools/host_path_bench.py ARGS (tools/trace_timeline.py)
@@ -84,6 +85,11 @@ for st in "$@"; do
       IFS=: read -r _ k nn c <<< "$st"
       timeout -k 10 300 python -u tools/dec_tstat.py $k $nn $c gibson_amd/liblzf_hip_time.so > $O/tstat_${k}_${nn}.txt 2>&1 || exit 1
       quiet $O/tstat_${k}_${nn}.txt ;;
+    kt:*)
+      # kt:K:N:C:LIB -- per-phase cycles of the table cand kernel (a -DKT_TIMING build gibson_amd/liblzf_hip_LIB.so)
+      IFS=: read -r _ k nn c lib <<< "$st"
+      LZF_HIP_LIB=$PWD/gibson_amd/liblzf_hip_$lib.so timeout -k 10 300 python -u tools/kt_timing.py $k $nn $c > $O/kt_${lib}_${k}_${nn}.txt 2>&1 || exit 1
+      quiet $O/kt_${lib}_${k}_${nn}.txt ;;
     xo:*)
       IFS=: read -r _ k nn c cs <<< "$st"
       XO_COUNTS=$cs timeout -k 10 600 python -u tools/crossover.py $k $nn $c > $O/xo_${k}_${nn}.txt 2>&1 || exit 1

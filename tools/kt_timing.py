@@ -7,8 +7,8 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["LZF_HIP_LIB"] = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gibson_amd",
-                                         "liblzf_hip_timing.so")
+os.environ.setdefault("LZF_HIP_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gibson_amd",
+                                         "liblzf_hip_timing.so"))
 os.environ.setdefault("LZF_GPU_TABLE_STAGE", "1")
 os.environ.setdefault("LZF_GPU_LANE_MIN", "0")
 import torch  # noqa: E402
