@@ -793,7 +793,8 @@ void host_batch(Ctx &c, const HostArgs &a, const View &v)
         host_batch_small(c, a, v);
 }
 
-/* a sub-batch on one context, failures as a return code */
+/* a sub-batch on one context, failures as a return code (a host allocation
+ * or thread-creation failure too: nothing may escape into the server) */
 int host_run(Ctx &c, const HostArgs &a, const View &v)
 {
     try {
@@ -802,6 +803,9 @@ int host_run(Ctx &c, const HostArgs &a, const View &v)
     } catch (const LzfFail &f) {
         c.quiesce();
         return f.code;
+    } catch (...) {
+        c.quiesce();
+        return LZF_GPU_ENOMEM;
     }
 }
 
@@ -954,12 +958,20 @@ int dispatch(uint32_t count, const std::function<int(Ctx &, const View &)> &job)
             rc = job(caller_ctx(), View{0, 1, count});
         } catch (const LzfFail &f) {
             rc = f.code;
+        } catch (...) {
+            rc = LZF_GPU_ENOMEM;
         }
         g_spread[0].values = count;
         g_spread[0].ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         return rc;
     }
-    std::vector<Worker *> &w = workers();
+    std::vector<Worker *> *wp = nullptr;
+    try {
+        wp = &workers();
+    } catch (...) {
+        return LZF_GPU_ENOMEM;                     /* a worker thread could not be made */
+    }
+    std::vector<Worker *> &w = *wp;
     Join j;
     j.left = G;
     for (uint32_t d = 0; d < G; d++) {
@@ -979,6 +991,8 @@ int dispatch(uint32_t count, const std::function<int(Ctx &, const View &)> &job)
                 rc = job(*c, v);
             } catch (const LzfFail &f) {
                 rc = f.code;
+            } catch (...) {
+                rc = LZF_GPU_ENOMEM;
             }
             sp->ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             j.done(rc);
@@ -1061,6 +1075,9 @@ int lzf_host_decoded_size_batch(const uint8_t *in, const uint64_t *in_off, const
         } catch (const LzfFail &f) {
             c.quiesce();
             return f.code;
+        } catch (...) {
+            c.quiesce();
+            return LZF_GPU_ENOMEM;
         }
     });
 }
@@ -1069,25 +1086,31 @@ int lzf_host_register(const void *ptr, uint64_t len)
 {
     if (!ptr || !len) return LZF_GPU_EARG;
     const uintptr_t lo = (uintptr_t)ptr, hi = lo + len;
+    const Plan &P = plan();
+    if (P.rc != LZF_GPU_OK) return P.rc;
+    /* the range is reserved as [lo, lo) while hipHostRegister runs outside
+     * the lock (no batch span fits an empty range, and an overlapping or
+     * second registration of it is refused), then entered whole */
     {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         auto it = g_reg.upper_bound(lo);
         if (it != g_reg.end() && it->first < hi) return LZF_GPU_EARG;          /* overlaps a later range */
         if (it != g_reg.begin() && std::prev(it)->second > lo) return LZF_GPU_EARG;
+        if (g_reg.count(lo)) return LZF_GPU_EARG;                               /* being registered */
+        g_reg[lo] = lo;
     }
-    const Plan &P = plan();
-    if (P.rc != LZF_GPU_OK) return P.rc;
     int prev = -1;
     (void)hipGetDevice(&prev);
-    if (hipSetDevice(P.dev[0]) != hipSuccess) return LZF_GPU_ENODEV;
+    hipError_t e = hipSetDevice(P.dev[0]);
     /* portable: every device of the plan maps it */
-    const hipError_t e = hipHostRegister((void *)ptr, len, hipHostRegisterMapped | hipHostRegisterPortable);
+    if (e == hipSuccess) e = hipHostRegister((void *)ptr, len, hipHostRegisterMapped | hipHostRegisterPortable);
     if (prev >= 0 && prev != P.dev[0]) (void)hipSetDevice(prev);
+    std::lock_guard<std::mutex> lk(g_reg_mu);
     if (e != hipSuccess) {
         (void)hipGetLastError();
+        g_reg.erase(lo);
         return code_of(e);
     }
-    std::lock_guard<std::mutex> lk(g_reg_mu);
     g_reg[lo] = hi;
     return LZF_GPU_OK;
 }
@@ -1097,7 +1120,7 @@ int lzf_host_unregister(const void *ptr)
     {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         auto it = g_reg.find((uintptr_t)ptr);
-        if (it == g_reg.end()) return LZF_GPU_EARG;
+        if (it == g_reg.end() || it->second == it->first) return LZF_GPU_EARG;   /* unknown, or being registered */
         g_reg.erase(it);
     }
     return hipHostUnregister((void *)ptr) == hipSuccess ? LZF_GPU_OK : LZF_GPU_ELAUNCH;

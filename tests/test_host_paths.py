@@ -216,3 +216,20 @@ def test_registered_bulk_chunks_config1_digest(digests_full, registered):
     gibson_amd.host_compress_batch(arena, off, np.full(count, n, np.uint32), out, off,
                                    np.full(count, n - 4, np.uint32), olen)
     assert batch_digest(out, n, olen) == digests_full[(kind, seed, n, count)]
+
+
+def test_bad_device_plan_is_reported_not_aborted():
+    # an LZF_GPU_DEVICES entry past the machine's devices: every host call
+    # returns LZF_GPU_ENODEV (the plan is read once, in a child process)
+    code = ("import numpy as np, gibson_amd\n"
+            "a = np.zeros(8192, np.uint8); o = np.zeros(8192, np.uint8)\n"
+            "off = np.zeros(1, np.uint64); ln = np.full(1, 8192, np.uint32); cap = np.full(1, 8188, np.uint32)\n"
+            "ol = np.zeros(1, np.uint32)\n"
+            "L = gibson_amd.lib()\n"
+            "p = lambda x: x.ctypes.data\n"
+            "print(L.lzf_host_compress_batch(p(a), p(off), p(ln), p(o), p(off), p(cap), p(ol), 1))\n"
+            "print(L.lzf_gpu_device_plan(None, None, None, 0))\n")
+    env = dict(os.environ, LZF_GPU_DEVICES="0,63")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.split() == ["-3", "-3"], r.stdout
