@@ -242,10 +242,14 @@ struct Slot {
     Buf h_in{nullptr, 0, true}, h_out{nullptr, 0, true}, h_meta{nullptr, 0, true};
     void *scratch = nullptr;       /* the slot's own compress scratch (registered path) */
     hipEvent_t in_done = nullptr;  /* the chunk's inputs are on the device (registered path) */
+    hipEvent_t out_done = nullptr; /* the chunk's outputs are in host memory (registered path) */
     uint32_t first = 0, count = 0;
     bool busy = false;
 };
 constexpr uint32_t NSLOT = 3;      /* registered path: chunks in flight */
+#ifndef CHAIN_OUT
+#define CHAIN_OUT 1                /* registered path: chunk outputs cross the bus in order */
+#endif
 
 struct Ctx {
     int dev = 0;
@@ -395,6 +399,7 @@ void make_slot_streams(Ctx &c)
         if (!sl.done) check(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming), "hipEventCreate");
         if (!sl.scratch) sl.scratch = lzf_scratch_create();
         if (!sl.in_done) check(hipEventCreateWithFlags(&sl.in_done, hipEventDisableTiming), "hipEventCreate");
+        if (!sl.out_done) check(hipEventCreateWithFlags(&sl.out_done, hipEventDisableTiming), "hipEventCreate");
         sl.busy = false;
     }
 }
@@ -612,7 +617,10 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
             bulk = true;
         }
     } else {
-        nchunks = (uint32_t)((total + (256ull << 20) - 1) / (256ull << 20));
+        uint64_t dchunk = 256ull << 20;
+        if (const char *e = getenv("LZF_GPU_HOST_DCHUNK_MB")) dchunk = (uint64_t)strtoull(e, nullptr, 10) << 20;
+        if (dchunk < (1u << 20)) dchunk = 1u << 20;
+        nchunks = (uint32_t)((total + dchunk - 1) / dchunk);
     }
     if (nchunks > v.count) nchunks = v.count;
     if (nchunks < 1) nchunks = 1;
@@ -659,11 +667,34 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         oruns.clear();
         uint64_t x = 0, y = 0;
         uint32_t max_len = 0;
+        /* a decode chunk whose inputs' whole span is no larger than its
+         * outputs goes H2D as that one span, gaps included: the bus's H2D
+         * side idles while the D2H side carries the decoded bytes, and a GPU
+         * gather's read requests would slow that D2H side */
+        bool span = false;
+        uint64_t slo = ~0ull, shi = 0;
+        if (!a.compress) {
+            uint64_t outb = 0;
+            for (uint32_t k = 0; k < n; k++) {
+                const uint32_t i = v.at(k0 + k);
+                const uint64_t so = a.in_off[i], ext = in_extent(a, i);
+                if (so < slo) slo = so;
+                if (so + ext > shi) shi = so + ext;
+                outb += a.out_cap[i];
+            }
+            span = n > 1u && shi - slo <= outb;
+            if (span) {
+                x = ((uintptr_t)in_map + slo) & 15u;
+                iruns.push_back(Run{slo, x, shi - slo});
+            }
+        }
         for (uint32_t k = 0; k < n; k++) {
             const uint32_t i = v.at(k0 + k);
             const uint64_t so = a.in_off[i], ext = in_extent(a, i);
-            if (!iruns.empty() && so >= iruns.back().host + iruns.back().len &&
-                so - (iruns.back().host + iruns.back().len) <= 256u) {
+            if (span) {
+                m_din[k] = iruns[0].dev + (so - slo);
+            } else if (!iruns.empty() && so >= iruns.back().host + iruns.back().len &&
+                       so - (iruns.back().host + iruns.back().len) <= 256u) {
                 Run &r = iruns.back();
                 m_din[k] = r.dev + (so - r.host);
                 if (so + ext - r.host > r.len) r.len = so + ext - r.host;
@@ -672,7 +703,7 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
                 iruns.push_back(Run{so, x, ext});
                 m_din[k] = x;
             }
-            if (m_din[k] + ext > x) x = m_din[k] + ext;
+            if (m_din[k] + ext > x) x = m_din[k] + ext;           /* span: x ends at the span's end */
             const uint64_t oo = a.out_off[i];
             if (!a.compress && !oruns.empty() && oo == oruns.back().host + oruns.back().len) {
                 Run &r = oruns.back();
@@ -726,6 +757,11 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         b.count = n;
         b.max_len = max_len;
         check(bulk ? lzf_route_compress_bulk(b, sl.stream, sl.scratch) : launch(a, b, sl.stream), "kernel launch");
+        /* outputs cross the bus in chunk order too: side by side, the chunks
+         * in flight would share the link and finish together, leaving it idle
+         * while the next ones gather and decode */
+        if (round && CHAIN_OUT)
+            check(hipStreamWaitEvent(sl.stream, c.slot[(round - 1) % NSLOT].out_done, 0), "hipStreamWaitEvent");
         if (!a.compress && oruns.size() <= few) {
             for (const Run &r : oruns)
                 if (r.len)
@@ -734,6 +770,7 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         } else {
             check(lzf_launch_move(d_out, d_dout, out_map, d_dst, d_out_len, 0u, n, sl.stream), "scatter launch");
         }
+        check(hipEventRecord(sl.out_done, sl.stream), "hipEventRecord");
         check(hipMemcpyAsync(h_meta + res_off, d_meta + res_off, (size_t)n * mrec - res_off, hipMemcpyDeviceToHost,
                              sl.stream),
               "hipMemcpyAsync");

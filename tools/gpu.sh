@@ -20,6 +20,7 @@
 #   kt:K:N:C:LIB        per-phase cycles of the table cand kernel (-DKT_TIMING build liblzf_hip_LIB.so)
 #   xo:K:N:C:COUNTS     routed generation vs window64 by batch size (tools/crossover.py)
 #   host[:reg]          PCIe-inclusive host-path rates (tools/host_path_bench.py); :reg registered only
+#   hostenv:LABEL:ENV:ARGS  tools/host_path_bench.py ARGS under ENV
 #   trace:LABEL:ARGS    kernel + copy timeline of tools/host_path_bench.py ARGS (tools/trace_timeline.py)
 #   gpus2               the N-rank bench path rehearsed with two ranks on the one device (gloo)
 #   calib               FETCH_SIZE / WRITE_SIZE calibration (tools/fetch_calib.hip, built as tools/fetch_calib_bin)
@@ -102,6 +103,11 @@ for st in "$@"; do
         fi
         timeout -k 10 300 python tools/host_path_bench.py $1 $2 $3 5 --register > $O/host_$4_reg.json 2> $O/host_$4_reg.err || exit 1
         cut -c1-300 $O/host_$4_reg.json; done ;;
+    hostenv:*)
+      # hostenv:LABEL:ENV:ARGS -- tools/host_path_bench.py ARGS under ENV (VAR=x,VAR2=y)
+      IFS=: read -r _ lab envs args <<< "$st"; args=${args//,/ }; envs=${envs//,/ }
+      env $envs timeout -k 10 300 python tools/host_path_bench.py $args > $O/host_$lab.json 2> $O/host_$lab.err || exit 1
+      python3 -c "import json;d=json.load(open('$O/host_$lab.json'));print('$lab', d['compress_GBps'], d['decompress_GBps'], d['roundtrip_GBps'], d['roundtrip_ok'])" ;;
     trace:*)
       IFS=: read -r _ lab args <<< "$st"; args=${args//,/ }
       timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/trace_$lab -o run -- python3 tools/host_path_bench.py $args > $O/trace_$lab.log 2>&1 || exit 1
