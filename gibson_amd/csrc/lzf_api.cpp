@@ -384,6 +384,8 @@ hipError_t lzf_route_compress(const LzfBatch &b, hipStream_t s) { return launch_
 hipError_t lzf_route_decompress(const LzfBatch &b, hipStream_t s) { return launch_decompress(b, s); }
 uint32_t lzf_route_min_count(uint32_t max_len) { return lane_min_count(max_len); }
 bool lzf_device_ok(int dev) { return device_ok(dev); }
+hipError_t lzf_route_compress_window(const LzfBatch &b, hipStream_t s) { return lzf_launch_compress(b, s); }
+bool lzf_route_default(void) { return kernel_gen() == GEN_TABLE && lds_order_ok(); }
 hipError_t lzf_route_compress_bulk(const LzfBatch &b, hipStream_t s, void *scratch)
 {
     return launch_compress(b, s, (Scratch *)scratch, true);

@@ -604,7 +604,12 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
     /* per value: src_off, d_in_off, d_out_off, dst_off (u64), in_len, out_cap, out_len, err (u32) */
     const size_t mrec = 4 * sizeof(uint64_t) + 4 * sizeof(uint32_t);
     uint64_t total = 0;
-    for (uint32_t k = 0; k < v.count; k++) total += a.compress ? a.in_len[v.at(k)] : a.out_cap[v.at(k)];
+    uint32_t max_len_all = 0;
+    for (uint32_t k = 0; k < v.count; k++) {
+        const uint32_t l = a.compress ? a.in_len[v.at(k)] : a.out_cap[v.at(k)];
+        total += l;
+        if (l > max_len_all) max_len_all = l;
+    }
     uint32_t nchunks = 1;
     bool bulk = false;
     if (a.compress) {
@@ -629,7 +634,30 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
      * 202 -> 211 ms, json4k 62 -> 66 -- its cand squeezes between running
      * parses either way, and the parse's floor does not shrink with it) */
     std::vector<uint32_t> bound;
-    for (uint32_t k = 0; k <= nchunks; k++) bound.push_back((uint32_t)((uint64_t)v.count * k / nchunks));
+    /* Tail mode (compress, values over 16 KiB): the first part of the batch
+     * goes through the routed generations as one chunk, whose parse -- a
+     * per-value chain of ~70 ms for 64 KiB values whatever the count --
+     * starts as soon as that part is in; the rest is compressed by window64
+     * (one wave per value, no such floor) in chunks as its input arrives,
+     * beside that parse.  Without it every routed chunk's floor starts after
+     * its own input, the last one after all of it.  The
+     * routed part's share: LZF_GPU_HOST_TAIL (percent of the values, default
+     * 50; 0 turns the mode off). */
+    uint32_t tail_from = v.count;
+    if (bulk && max_len_all > 16384u && lzf_route_default()) {
+        uint32_t pct = 50u;
+        if (const char *e = getenv("LZF_GPU_HOST_TAIL")) pct = (uint32_t)strtoul(e, nullptr, 10);
+        if (pct > 0u && pct < 100u) tail_from = (uint32_t)((uint64_t)v.count * pct / 100u);
+    }
+    if (tail_from < v.count) {
+        const uint32_t TAIL_CHUNKS = 4u;
+        bound.push_back(0u);
+        bound.push_back(tail_from);
+        for (uint32_t k = 1; k <= TAIL_CHUNKS; k++)
+            bound.push_back(tail_from + (uint32_t)((uint64_t)(v.count - tail_from) * k / TAIL_CHUNKS));
+    } else {
+        for (uint32_t k = 0; k <= nchunks; k++) bound.push_back((uint32_t)((uint64_t)v.count * k / nchunks));
+    }
     const uint32_t min_len = a.compress ? 0u : 1u;
 
     auto drain = [&](Slot &sl) {
@@ -652,7 +680,13 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
     uint32_t round = 0;
     for (; round + 1 < bound.size(); round++) {
         const uint32_t k0 = bound[round], n = bound[round + 1] - k0;
-        Slot &sl = c.slot[round % NSLOT];
+        /* tail mode keeps slot 0 for the routed chunk (it finishes last) and
+         * rotates the window64 chunks over the others */
+        const uint32_t si = tail_from == v.count ? round % NSLOT : round == 0u ? 0u : 1u + (round - 1u) % (NSLOT - 1u);
+        const uint32_t prev_si = round == 0u ? 0u
+                                 : tail_from == v.count ? (round - 1u) % NSLOT
+                                 : round == 1u ? 0u : 1u + (round - 2u) % (NSLOT - 1u);
+        Slot &sl = c.slot[si];
         drain(sl);
         uint8_t *h_meta = (uint8_t *)sl.h_meta.get((size_t)n * mrec);
         uint64_t *m_src = (uint64_t *)h_meta, *m_din = m_src + n, *m_dout = m_din + n, *m_dst = m_dout + n;
@@ -735,7 +769,7 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         /* the chunks' inputs cross the bus one chunk after the other (side by
          * side they would share the link and all arrive at the end): chunk
          * k's kernels then start when its own inputs are in */
-        if (round) check(hipStreamWaitEvent(sl.stream, c.slot[(round - 1) % NSLOT].in_done, 0), "hipStreamWaitEvent");
+        if (round) check(hipStreamWaitEvent(sl.stream, c.slot[prev_si].in_done, 0), "hipStreamWaitEvent");
         if (iruns.size() <= few) {
             for (const Run &r : iruns)
                 if (r.len)
@@ -756,12 +790,17 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         b.err = (int32_t *)(d_out_len + n);
         b.count = n;
         b.max_len = max_len;
-        check(bulk ? lzf_route_compress_bulk(b, sl.stream, sl.scratch) : launch(a, b, sl.stream), "kernel launch");
+        const bool tail = k0 >= tail_from;
+        check(tail   ? lzf_route_compress_window(b, sl.stream)
+              : bulk ? lzf_route_compress_bulk(b, sl.stream, sl.scratch)
+                     : launch(a, b, sl.stream),
+              "kernel launch");
         /* outputs cross the bus in chunk order too: side by side, the chunks
          * in flight would share the link and finish together, leaving it idle
-         * while the next ones gather and decode */
-        if (round && CHAIN_OUT)
-            check(hipStreamWaitEvent(sl.stream, c.slot[(round - 1) % NSLOT].out_done, 0), "hipStreamWaitEvent");
+         * while the next ones gather and decode (not in tail mode: the
+         * routed chunk finishes last) */
+        if (round && CHAIN_OUT && tail_from == v.count)
+            check(hipStreamWaitEvent(sl.stream, c.slot[prev_si].out_done, 0), "hipStreamWaitEvent");
         if (!a.compress && oruns.size() <= few) {
             for (const Run &r : oruns)
                 if (r.len)
@@ -779,7 +818,7 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         sl.count = n;
         sl.busy = true;
     }
-    for (uint32_t k = 0; k < NSLOT; k++) drain(c.slot[(round + k) % NSLOT]);
+    for (uint32_t k = 0; k < NSLOT; k++) drain(c.slot[k]);
 }
 
 /* the [lo, hi) byte ranges a sub-batch reads and writes in the caller's arenas */

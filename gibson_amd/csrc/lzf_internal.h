@@ -117,6 +117,10 @@ void lzf_scratch_release_all(void);
 /* compress with the routed generations whatever the batch size, on a private
  * scratch (lzf_scratch_create): the host pipeline's side-by-side chunks */
 hipError_t lzf_route_compress_bulk(const LzfBatch &b, hipStream_t s, void *scratch);
+/* window64 (one wave per value), and whether the default routing is in
+ * force (no LZF_GPU_KERNEL override, the LDS lane order held) */
+hipError_t lzf_route_compress_window(const LzfBatch &b, hipStream_t s);
+bool lzf_route_default(void);
 void *lzf_scratch_create(void);
 void lzf_scratch_release(void *scratch);
 void lzf_scratch_destroy(void *scratch);

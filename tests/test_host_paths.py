@@ -233,3 +233,30 @@ def test_bad_device_plan_is_reported_not_aborted():
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.split() == ["-3", "-3"], r.stdout
+
+
+def test_registered_tail_mode_64k(oracle, registered):
+    # 256 MiB of 64 KiB values (configs[2]'s generator): the registered path's
+    # tail mode -- half the values through the table generation, the rest by
+    # window64 in chunks beside its parse -- against the staged path and a
+    # sample of the oracle
+    import gibson_amd
+    from tests.oracle_lib import _SYN
+    n, count = 65536, 4096
+    arena = registered(_aligned(count * n))
+    _SYN.synth_fill(2, 0x5EED0003, 0, count, n, arena.ctypes.data)
+    off = np.arange(count, dtype=np.uint64) * n
+    ln = np.full(count, n, np.uint32)
+    cap = np.full(count, n - 4, np.uint32)
+    out_r = registered(_aligned(count * n))
+    olen_r = np.zeros(count, np.uint32)
+    gibson_amd.host_compress_batch(arena, off, ln, out_r, off, cap, olen_r)
+    out_s = np.zeros(count * n, np.uint8)
+    olen_s = np.zeros(count, np.uint32)
+    gibson_amd.host_compress_batch(arena, off, ln, out_s, off, cap, olen_s)
+    assert np.array_equal(olen_r, olen_s)
+    for i in range(count):
+        assert np.array_equal(out_r[i * n:i * n + olen_r[i]], out_s[i * n:i * n + olen_s[i]]), i
+    for i in list(range(0, count, 97)) + [count // 2 - 1, count // 2, count - 1]:
+        exp = oracle.compress(bytes(arena[i * n:(i + 1) * n]), n - 4)
+        assert bytes(out_r[i * n:i * n + olen_r[i]]) == exp, i
