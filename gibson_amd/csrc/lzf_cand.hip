@@ -388,14 +388,30 @@ __global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt,
 #endif
 
 /* rel codes of the walk, relative to p: the record codes 0..7, plus
- * 8 (the first 3 bytes agree, length unknown) and 9 (unknown) */
+ * 8 (the first 3 bytes agree, length unknown) and 9 (unknown).
+ * K3_EXACT (round 5): exact agreements combine too.  If p~q agree in exactly
+ * a bytes and q~r in exactly b != a, then p~r agree in exactly min(a, b) (the
+ * first mismatch of the shorter one is a mismatch of p~r, the bytes before
+ * it agree in all three); with one of them exact (a < 8) and the other
+ * >= 8, exactly the exact one; both >= 8, >= 8.  A deeper candidate's match
+ * length then often needs no extension load (a record's agreements are capped
+ * at its own remaining bytes, which are more than p's: the cap binds p's
+ * first, so the rule holds at the value's end too). */
+#ifndef K3_EXACT
+#define K3_EXACT 1
+#endif
 __device__ __forceinline__ uint32_t k3_comb(uint32_t rel, uint32_t code)
 {
     /* p~q agree in 3 bytes and q~r agree in 3 bytes => p~r agree in 3;
      * exactly one of them => p~r differ in the first 3 bytes */
     if (rel == 9u) return 9u;
     const bool e1 = rel >= 2u, e2 = code >= 2u;
-    return (e1 && e2) ? 8u : (e1 != e2) ? RC_DIFF : 9u;
+    if (!(e1 && e2)) return (e1 != e2) ? RC_DIFF : 9u;
+    if (K3_EXACT && rel <= RC_LONG) {              /* rel exact (2..6) or >= 8 (7); code is 2..7 */
+        if (rel != code) return rel < code ? rel : code;   /* min: an exact one below the other */
+        if (rel == RC_LONG) return RC_LONG;        /* both >= 8 */
+    }
+    return 8u;
 }
 
 enum { K3_STEP = 0, K3_RESOLVE = 1, K3_DECIDE = 2, K3_EXTEND = 3, K3_EMIT = 4, K3_DONE = 5 };
