@@ -80,6 +80,20 @@ __device__ __forceinline__ uint4 cd_ld16(const uint8_t *p, uint32_t avail)
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+/* v shifted down by d bytes (0 < d < 16), zeros in from the top */
+__device__ __forceinline__ uint4 cd_shr16(uint4 v, uint32_t d)
+{
+    uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
+    if (d >= 8u) {
+        lo = hi >> (8u * (d - 8u));
+        hi = 0u;
+    } else {
+        lo = (lo >> (8u * d)) | (hi << (64u - 8u * d));
+        hi >>= 8u * d;
+    }
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+
 /* the wave's lane mask of a predicate, straight from the compare (HIP's
  * __ballot takes an int, which can cost a select and a compare per use) */
 __device__ __forceinline__ uint64_t cd_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
@@ -93,7 +107,11 @@ __device__ __forceinline__ void cd_fence()
 #ifdef CD_TIMING
 /* diagnostic build: per role, cycles working and cycles waiting at the
  * pipe's barriers, summed over waves (lzf_gpu_dec_tstat) */
-__device__ unsigned long long cd_tstat[8];
+/* 1024 rows of 8 counters, a workgroup adding to row blockIdx.x % 1024: one
+ * row for all would serialise ~6 atomics per workgroup at one L2 channel
+ * (1 M values of 8 KiB: 88 ms instead of 15) */
+#define CD_TROWS 1024u
+__device__ unsigned long long cd_tstat[CD_TROWS * 8u];
 #endif
 
 /* workgroup barrier with LDS release/acquire (the pipe's hand-over); tw[0]
@@ -173,6 +191,12 @@ __device__ __forceinline__ void cd_stage(uint8_t *inr, const uint8_t *src, uint3
 #ifndef CD_PREF
 #define CD_PREF 1
 #endif
+/* the pipe producer's input pieces two rounds ahead (round 5; the kernel) */
+#ifndef CD_PREF2
+#define CD_PREF2 1
+#endif
+template <uint32_t V> struct CdPar { static constexpr uint32_t value = V; };
+__device__ uint4 cd_dummy16;    /* the idle lanes' load address */
 /* CD_CPRIO: issue priority of the pipe's consumer wave (s_setprio).  VALU
  * issue is arbitrated by priority, then age; with the consumer first: Zipf
  * 16.14 -> 15.57 ms, sentence text 12.79 -> 12.10, mixed 7.93 -> 7.99 (the
@@ -588,7 +612,7 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
     const uint32_t in_len = __builtin_amdgcn_readfirstlane(bt.in_len[v]);   /* scalar: no load wait in the loop */
     const uint32_t cap = __builtin_amdgcn_readfirstlane(bt.out_cap[v]);
 
-    uint64_t tw[3] = {0ull, 0ull, 0ull};
+    uint64_t tw[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
 #ifdef CD_TIMING
     tw[2] = __builtin_amdgcn_s_memtime();
 #endif
@@ -606,8 +630,41 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
         uint4 pv = make_uint4(0u, 0u, 0u, 0u);
         uint32_t pto = 0u;
         bool pend = false;
-        for (uint32_t k = 0;; k++) {
-            if (CD_PREF && pend) {
+        /* CD_PREF2: two rounds ahead.  The piece issued in round k lands in
+         * register set k & 1 and is written at round k + 2's start, so a load
+         * has two rounds to land.  It reaches base_k + 608, whose ring slot is
+         * base_k + 96 < base_{k+1}: the consumer, then in round k + 1, has
+         * left it (bases advance >= 128 per round but the last).  The loop is
+         * unrolled by two so each set is its own registers: a select between
+         * the sets would wait for the one in flight */
+        uint4 pq0 = make_uint4(0u, 0u, 0u, 0u), pq1 = pq0;
+        uint32_t pf0 = 0u, pt0 = 0u, pf1 = 0u, pt1 = 0u, iss = 0u;
+        auto round = [&](auto par, uint32_t k) -> bool {
+            constexpr uint32_t P = decltype(par)::value;
+#ifdef CD_TIMING
+            const uint64_t ts0 = __builtin_amdgcn_s_memtime();
+#endif
+            if (CD_PREF2) {
+                uint4 &q = P ? pq1 : pq0;
+                uint32_t &qf = P ? pf1 : pf0, &qt = P ? pt1 : pt0;
+                {
+                    /* no uniform branch around the write or the load below: the
+                     * compiler's wait counting then sees one load per set per
+                     * two rounds and waits for this set's alone */
+                    const uint32_t px = qf + 16u * lane;
+                    if (px < qt) {
+                        /* the stream's last piece was loaded from avail - 16:
+                         * its bytes move down by d, zeros above avail */
+                        const uint32_t d = qt - px < 16u ? 16u - (qt - px) : 0u;
+                        uint4 w = q;
+                        if (d) w = cd_shr16(w, d);
+                        *(uint4 *)(inr + (px & (CD_IN_RINGP - 1u))) = w;
+                    }
+                    loaded = max(loaded, qt);
+                    qf = qt = 0u;
+                    cd_fence();
+                }
+            } else if (CD_PREF && pend) {
                 const uint32_t px = loaded + 16u * lane;
                 if (px < pto) {
                     *(uint4 *)(inr + (px & (CD_IN_RINGP - 1u))) = pv;
@@ -617,22 +674,52 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
                 cd_fence();
             }
             cd_stage_pipe(inr, src, base, avail, loaded, lane);
-            /* the next round starts at >= base + 128 (tokens start in
-             * [base, base + 128) and the last one ends past it) and at most
-             * base + 160: the ring may take up to base + 448 at its start
-             * (the consumer then reads round k's [base, base + 161), and
-             * offset y overwrites y - 512), and needs base_{k+1} + 192 */
-            if (CD_PREF && loaded < min(avail, base + 448u) && base + 128u < in_len) {
+            if (CD_PREF2) {
+                uint4 &q = P ? pq1 : pq0;
+                uint32_t &qf = P ? pf1 : pf0, &qt = P ? pt1 : pt0;
+                iss = max(iss, loaded);
+                const uint32_t lim = min(avail, (base + 608u) & ~15u);
+                const bool go = iss < lim && base + 128u < in_len;
+                /* one 16-byte load per lane every round, the last piece's from
+                 * avail - 16 (in_len > 128 when go), idle lanes' from a dummy:
+                 * no byte loop and no branch, so the load stays in flight for
+                 * two rounds */
+                const uint32_t px = iss + 16u * lane;
+                const uint8_t *pa = (go && px < lim) ? src + (lim - px >= 16u ? px : avail - 16u)
+                                                     : (const uint8_t *)&cd_dummy16;
+                __builtin_memcpy(&q, pa, 16);
+                qf = go ? iss : 0u;
+                qt = go ? lim : 0u;
+                iss = go ? lim : iss;
+            } else if (CD_PREF && loaded < min(avail, base + 448u) && base + 128u < in_len) {
+                /* the next round starts at >= base + 128 (tokens start in
+                 * [base, base + 128) and the last one ends past it) and at most
+                 * base + 160: the ring may take up to base + 448 at its start
+                 * (the consumer then reads round k's [base, base + 161), and
+                 * offset y overwrites y - 512), and needs base_{k+1} + 192 */
                 pto = min(avail, (base + 448u) & ~15u);
                 const uint32_t px = loaded + 16u * lane;
                 if (px < pto) pv = cd_ld16(src + px, pto - px);
                 pend = true;
             }
+#ifdef CD_TIMING
+            const uint64_t td0 = __builtin_amdgcn_s_memtime();
+#endif
             const uint32_t x = cd_discover_lds(inr, imask, jt, base, in_len, lane);
+#ifdef CD_TIMING
+            const uint64_t td1 = __builtin_amdgcn_s_memtime();
+#endif
             const CdRound r = cd_decode(inr, imask, base, x, O, in_len, cap);
+#ifdef CD_TIMING
+            /* the producer's parts: staging, token discovery, token decode (the
+             * latter ends at a use of its results, so its waits are in it) */
+            tw[3] += td1 - td0;
+            tw[5] += td0 - ts0;
+            tw[4] += __builtin_amdgcn_s_memtime() - td1;
+#endif
             const uint32_t ntok = r.ntok;
             const uint32_t total = r.total;
-            CdSlot &s = slot[k & 1u];
+            CdSlot &s = slot[P];
             s.tok[lane] = (r.tinfo << 17) | ((r.tinfo >> 31) << 16) | r.rel;   /* rel < 65536 */
             const bool last = r.err != 0 || r.nbase >= in_len;   /* src/lzf_d.c:146 */
             if (lane == 0) {
@@ -644,7 +731,12 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
             O += total;
             base = r.nbase;
             cd_barrier(tw);
-            if (last) break;
+            (void)k;
+            return last;
+        };
+        for (uint32_t k = 0;; k += 2u) {
+            if (round(CdPar<0>(), k)) break;
+            if (round(CdPar<1>(), k + 1u)) break;
         }
     } else {
         uint8_t *dst = bt.out + bt.out_off[v];
@@ -686,8 +778,14 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
     }
 #ifdef CD_TIMING
     if (lane == 0) {
-        atomicAdd(&cd_tstat[producer ? 0 : 2], (unsigned long long)tw[0]);
-        atomicAdd(&cd_tstat[producer ? 1 : 3], (unsigned long long)tw[1]);
+        const uint32_t tr = (blockIdx.x % CD_TROWS) * 8u;
+        atomicAdd(&cd_tstat[tr + (producer ? 0 : 2)], (unsigned long long)tw[0]);
+        atomicAdd(&cd_tstat[tr + (producer ? 1 : 3)], (unsigned long long)tw[1]);
+        if (producer) {
+            atomicAdd(&cd_tstat[tr + 4], (unsigned long long)tw[3]);
+            atomicAdd(&cd_tstat[tr + 5], (unsigned long long)tw[4]);
+            atomicAdd(&cd_tstat[tr + 6], (unsigned long long)tw[5]);
+        }
     }
 #endif
 }
@@ -729,8 +827,13 @@ hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s)
  * summed over waves since the last call) */
 extern "C" int lzf_gpu_dec_tstat(unsigned long long *out)
 {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cd_tstat), sizeof(cd_tstat)) != hipSuccess) return -1;
-    static const unsigned long long z[8] = {0};
+    static unsigned long long rows[CD_TROWS * 8u];
+    if (hipMemcpyFromSymbol(rows, HIP_SYMBOL(cd_tstat), sizeof(rows)) != hipSuccess) return -1;
+    for (uint32_t i = 0; i < 8u; i++) {
+        out[i] = 0;
+        for (uint32_t r = 0; r < CD_TROWS; r++) out[i] += rows[8u * r + i];
+    }
+    static const unsigned long long z[CD_TROWS * 8u] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(cd_tstat), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

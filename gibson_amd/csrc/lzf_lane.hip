@@ -939,6 +939,31 @@ extern "C" int lzf_gpu_debug_sites(unsigned long long *out16, int reset)
 #endif
 enum { K2_STEP = 0, K2_RESOLVE = 1, K2_DECIDE = 2, K2_EXTEND = 3, K2_EMIT = 4, K2_DONE = 5 };
 
+/* rel of p to the next link r of the chain from its rel to q and q's cand
+ * code for r.  3-byte agreements combine (both agree => p~r agree, exactly one
+ * => they differ); K2_EXACT: exact agreements too -- p~q exactly a bytes and
+ * q~r exactly b != a give p~r exactly min(a, b), one exact and one >= 8 give
+ * the exact one, both >= 8 give >= 8 (cand words are capped at their own
+ * remaining bytes, more than p's, so the rule holds at the value's end; the
+ * same rule as lzf_cand.hip's k3_comb) */
+/* off by default: same-process A/B, output identical (profiles/r05/cand/ab_k2x*):
+ * json4k 47.21 -> 47.49 ms, mixed16k 50.56 -> 50.96, text8k 48.03 -> 47.77 --
+ * lane generation's chains are short and its agreement probes are LDS-cheap */
+#ifndef K2_EXACT
+#define K2_EXACT 0
+#endif
+__device__ __forceinline__ uint32_t k2_comb(uint32_t rel, uint32_t code)
+{
+    if (rel == 9u) return 9u;
+    const bool e1 = rel >= 2u, e2 = code >= 2u;
+    if (!(e1 && e2)) return (e1 != e2) ? CAND_DIFF : 9u;
+    if (K2_EXACT && rel <= CAND_LONG) {
+        if (rel != code) return rel < code ? rel : code;
+        if (rel == CAND_LONG) return CAND_LONG;
+    }
+    return 8u;
+}
+
 __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt, LzfLaneScratch sc)
 {
     const uint32_t v = blockIdx.x * K2_THREADS + threadIdx.x;
@@ -1128,8 +1153,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                         rel = 0u;
                         mode = K2_DECIDE;
                     } else {
-                        const bool e1 = rel >= 2u && rel <= 8u, e2 = r2 >= 2u;
-                        rel = rel == 9u ? 9u : (e1 && e2) ? 8u : (e1 != e2) ? 1u : 9u;
+                        rel = k2_comb(rel, r2);
                         q = q2;
                     }
                 }

@@ -85,7 +85,7 @@ for st in "$@"; do
       quiet $O/env_${k}_${nn}.txt ;;
     tstat:*)
       IFS=: read -r _ k nn c <<< "$st"
-      timeout -k 10 300 python -u tools/dec_tstat.py $k $nn $c gibson_amd/liblzf_hip_time.so > $O/tstat_${k}_${nn}.txt 2>&1 || exit 1
+      timeout -k 10 300 python -u tools/dec_tstat.py $k $nn $c gibson_amd/liblzf_hip.so gibson_amd/liblzf_hip_time.so > $O/tstat_${k}_${nn}.txt 2>&1 || exit 1
       quiet $O/tstat_${k}_${nn}.txt ;;
     kt:*)
       # kt:K:N:C:LIB -- per-phase cycles of the table cand kernel (a -DKT_TIMING build gibson_amd/liblzf_hip_LIB.so)
