@@ -642,10 +642,12 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
      * beside that parse.  Without it every routed chunk's floor starts after
      * its own input, the last one after all of it.  The
      * routed part's share: LZF_GPU_HOST_TAIL (percent of the values, default
-     * 50; 0 turns the mode off). */
+     * 60; 0 turns the mode off).  Registered text64k, 64 K values, compress
+     * GB/s by share: off 20.8, 30 % 21.6, 40 % 22.6, 50 % 23.9, 60 % 24.3,
+     * 70 % 24.3, 80 % 23.0, 90 % 21.7 (profiles/r05/host_text64k_reg_tail*). */
     uint32_t tail_from = v.count;
     if (bulk && max_len_all > 16384u && lzf_route_default()) {
-        uint32_t pct = 50u;
+        uint32_t pct = 60u;
         if (const char *e = getenv("LZF_GPU_HOST_TAIL")) pct = (uint32_t)strtoul(e, nullptr, 10);
         if (pct > 0u && pct < 100u) tail_from = (uint32_t)((uint64_t)v.count * pct / 100u);
     }
