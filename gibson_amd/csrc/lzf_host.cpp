@@ -247,6 +247,8 @@ struct Slot {
     bool busy = false;
 };
 constexpr uint32_t NSLOT = 3;      /* registered path: chunks in flight */
+constexpr uint32_t TAIL_MAX = 4;   /* tail mode: window64 chunks (at most), each with its own slot */
+constexpr uint32_t NSLOT_ALL = 1u + TAIL_MAX;
 #ifndef CHAIN_OUT
 #define CHAIN_OUT 1                /* registered path: chunk outputs cross the bus in order */
 #endif
@@ -258,7 +260,7 @@ struct Ctx {
     hipStream_t stream = nullptr;
     Buf d_in, d_out, d_meta;
     Buf h_in{nullptr, 0, true}, h_out{nullptr, 0, true}, h_meta{nullptr, 0, true};
-    Slot slot[NSLOT];
+    Slot slot[NSLOT_ALL];
     Ctx(int device, bool bound) : dev(device), numa_bound(bound)
     {
         int n = 0;
@@ -642,17 +644,23 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
      * beside that parse.  Without it every routed chunk's floor starts after
      * its own input, the last one after all of it.  The
      * routed part's share: LZF_GPU_HOST_TAIL (percent of the values, default
-     * 60; 0 turns the mode off).  Registered text64k, 64 K values, compress
-     * GB/s by share: off 20.8, 30 % 21.6, 40 % 22.6, 50 % 23.9, 60 % 24.3,
-     * 70 % 24.3, 80 % 23.0, 90 % 21.7 (profiles/r05/host_text64k_reg_tail*). */
+     * 70; 0 turns the mode off); window64 chunks: LZF_GPU_HOST_TAIL_CHUNKS
+     * (1-4, default 1).  Registered text64k, 64 K values, compress GB/s
+     * (profiles/r05/host_text64k_reg_tail*, tail_chunks/): four window
+     * chunks by share: off 20.8, 30 % 21.6, 40 % 22.6, 50 % 23.9, 60 % 24.3,
+     * 70 % 24.3, 80 % 23.0, 90 % 21.7; at 70 %, 1 / 2 / 3 / 4 chunks: 24.9 /
+     * 24.4 / 24.4 / 24.3; one chunk at 60 / 80 %: 23.0 / 23.1. */
     uint32_t tail_from = v.count;
     if (bulk && max_len_all > 16384u && lzf_route_default()) {
-        uint32_t pct = 60u;
+        uint32_t pct = 70u;
         if (const char *e = getenv("LZF_GPU_HOST_TAIL")) pct = (uint32_t)strtoul(e, nullptr, 10);
         if (pct > 0u && pct < 100u) tail_from = (uint32_t)((uint64_t)v.count * pct / 100u);
     }
     if (tail_from < v.count) {
-        const uint32_t TAIL_CHUNKS = 4u;
+        uint32_t TAIL_CHUNKS = 1u;
+        if (const char *e = getenv("LZF_GPU_HOST_TAIL_CHUNKS")) TAIL_CHUNKS = (uint32_t)strtoul(e, nullptr, 10);
+        if (TAIL_CHUNKS < 1u) TAIL_CHUNKS = 1u;
+        if (TAIL_CHUNKS > TAIL_MAX) TAIL_CHUNKS = TAIL_MAX;
         bound.push_back(0u);
         bound.push_back(tail_from);
         for (uint32_t k = 1; k <= TAIL_CHUNKS; k++)
@@ -682,12 +690,12 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
     uint32_t round = 0;
     for (; round + 1 < bound.size(); round++) {
         const uint32_t k0 = bound[round], n = bound[round + 1] - k0;
-        /* tail mode keeps slot 0 for the routed chunk (it finishes last) and
-         * rotates the window64 chunks over the others */
-        const uint32_t si = tail_from == v.count ? round % NSLOT : round == 0u ? 0u : 1u + (round - 1u) % (NSLOT - 1u);
-        const uint32_t prev_si = round == 0u ? 0u
-                                 : tail_from == v.count ? (round - 1u) % NSLOT
-                                 : round == 1u ? 0u : 1u + (round - 2u) % (NSLOT - 1u);
+        /* tail mode: slot 0 for the routed chunk (it finishes last), one slot
+         * each for the window64 chunks, so every chunk's input crosses the bus
+         * as soon as the one before it is in (with two slots for four chunks,
+         * the third waited for the first's kernel: profiles/r05/tail_chunks/) */
+        const uint32_t si = tail_from == v.count ? round % NSLOT : round;
+        const uint32_t prev_si = round == 0u ? 0u : tail_from == v.count ? (round - 1u) % NSLOT : round - 1u;
         Slot &sl = c.slot[si];
         drain(sl);
         uint8_t *h_meta = (uint8_t *)sl.h_meta.get((size_t)n * mrec);
@@ -820,7 +828,7 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         sl.count = n;
         sl.busy = true;
     }
-    for (uint32_t k = 0; k < NSLOT; k++) drain(c.slot[k]);
+    for (uint32_t k = 0; k < NSLOT_ALL; k++) drain(c.slot[k]);
 }
 
 /* the [lo, hi) byte ranges a sub-batch reads and writes in the caller's arenas */
