@@ -235,11 +235,16 @@ def test_bad_device_plan_is_reported_not_aborted():
     assert r.stdout.split() == ["-3", "-3"], r.stdout
 
 
-def test_registered_tail_mode_64k(oracle, registered):
+@pytest.mark.parametrize("share,chunks", [(None, None), (50, 4)], ids=["default", "50pct-4chunks"])
+def test_registered_tail_mode_64k(oracle, registered, monkeypatch, share, chunks):
     # 256 MiB of 64 KiB values (configs[2]'s generator): the registered path's
-    # tail mode -- half the values through the table generation, the rest by
-    # window64 in chunks beside its parse -- against the staged path and a
-    # sample of the oracle
+    # tail mode -- the first part of the values through the table generation,
+    # the rest by window64 in chunks beside its parse (default 70 % and one
+    # chunk; 50 % and four, each chunk in its own slot) -- against the staged
+    # path and a sample of the oracle that includes every chunk boundary
+    if share is not None:
+        monkeypatch.setenv("LZF_GPU_HOST_TAIL", str(share))
+        monkeypatch.setenv("LZF_GPU_HOST_TAIL_CHUNKS", str(chunks))
     import gibson_amd
     from tests.oracle_lib import _SYN
     n, count = 65536, 4096
@@ -257,6 +262,9 @@ def test_registered_tail_mode_64k(oracle, registered):
     assert np.array_equal(olen_r, olen_s)
     for i in range(count):
         assert np.array_equal(out_r[i * n:i * n + olen_r[i]], out_s[i * n:i * n + olen_s[i]]), i
-    for i in list(range(0, count, 97)) + [count // 2 - 1, count // 2, count - 1]:
+    pct, nch = (share or 70), (chunks or 1)
+    t = count * pct // 100
+    edges = [t + (count - t) * k // nch for k in range(nch)]
+    for i in sorted(set(list(range(0, count, 97)) + [e + d for e in edges for d in (-1, 0)] + [count - 1])):
         exp = oracle.compress(bytes(arena[i * n:(i + 1) * n]), n - 4)
         assert bytes(out_r[i * n:i * n + olen_r[i]]) == exp, i
