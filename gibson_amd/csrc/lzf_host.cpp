@@ -620,7 +620,10 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         if (chunk_bytes < (1u << 20)) chunk_bytes = 1u << 20;
         if (total >= (192ull << 20) && v.count >= NSLOT * 1024u) {
             nchunks = (uint32_t)((total + chunk_bytes - 1) / chunk_bytes);
-            if (nchunks < NSLOT) nchunks = NSLOT;
+            uint32_t nmin = NSLOT;
+            if (const char *e = getenv("LZF_GPU_HOST_NCHUNKS")) nmin = (uint32_t)strtoul(e, nullptr, 10);
+            if (nmin < 1u) nmin = 1u;
+            if (nchunks < nmin) nchunks = nmin;
             bulk = true;
         }
     } else {
