@@ -145,7 +145,22 @@ extern "C" int lzf_gpu_debug_kt(unsigned long long *out16, int reset)
     return e == hipSuccess ? 0 : -2;
 }
 #define KT_T0() uint64_t kt_t = __builtin_amdgcn_s_memtime()
-#define KT_TM(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); kt_acc[i] += t_ - kt_t; kt_t = t_; } while (0)
+#ifdef KT_LITE
+/* -DKT_LITE: each wave's busy cycles per step (step start to the barrier),
+ * written to kt_trace for the first KT_LW workgroups and KT_LS steps; no
+ * per-phase sums (the per-phase form spills ~95 VGPRs and runs the kernel
+ * ~3.5x slower, which skews its phase figures) */
+#define KT_LW 64u
+#define KT_LS 4096u
+__device__ uint32_t kt_trace[KT_LW * KT_LS * 16u];
+extern "C" int lzf_gpu_debug_kt_trace(uint32_t *out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(kt_trace), sizeof(kt_trace)) == hipSuccess ? 0 : -2;
+}
+#define KT_TM(i) ((void)0)
+#else
+#define KT_TM(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); kt_loc[i] += t_ - kt_t; kt_t = t_; } while (0)
+#endif
 #else
 #define KT_T0() ((void)0)
 #define KT_TM(i) ((void)0)
@@ -157,14 +172,38 @@ struct KtLds {
 };
 
 template <uint32_t V> struct KtIc { static constexpr uint32_t value = V; };
+/* KT_INTERIOR (round 5): the main loop's steps with their block and position
+ * tests dropped (they hold there); the first KT_PF steps keep them */
+#ifndef KT_INTERIOR
+#define KT_INTERIOR 1
+#endif
+/* KT_SPRE (round 5): workers store the table wave's exchange address */
+#ifndef KT_SPRE
+#define KT_SPRE 1
+#endif
 
+#ifdef KT_TIMING
+#define KT_ACC_ARG , uint64_t *kt_acc, uint32_t *kt_busy
+#define KT_ACC_PASS , kt_acc, kt_busy
+#else
+#define KT_ACC_ARG
+#define KT_ACC_PASS
+#endif
 template <bool SMALL>
-__device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uint32_t n, uint32_t *rec)
+__device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uint32_t n, uint32_t *rec KT_ACC_ARG)
 {
     uint16_t *const T = L.T, *const Q = L.Q, *const O = L.O;
     uint32_t *const S = L.S;
+#ifdef KT_WREV
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = KT_WIN - (tid >> 6);   /* experiment: table wave last */
+#else
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+#endif
+#ifdef KT_JREV
+    const uint32_t j = KT_WIN - w;                             /* experiment: windows in reverse wave order */
+#else
     const uint32_t j = w - 1u;                                 /* worker's window (w >= 1) */
+#endif
     const uint32_t np = n - 2u;                                /* positions 0 .. n-3, src/lzf_c.c:145 */
     const uint32_t nb = (np + KT_BLK - 1u) / KT_BLK;
     /* worker: the 8 bytes of its position in the next KT_PF blocks are in
@@ -202,16 +241,27 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
         c_a[i] = c_b1[i] = c_b2[i] = make_uint2(0u, 0u);
     }
 #ifdef KT_TIMING
-    uint64_t kt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t kt_loc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-    const auto step = [&](auto ps, auto clamp, uint32_t t) {
+    /* m3 = t % 3 (the O buffer of block t), kept by the caller: the three
+     * k % 3 of a step are selects of it, not three scalar divisions */
+    const auto step = [&](auto ps, auto clamp, uint32_t t, uint32_t m3) {
         constexpr uint32_t PS = decltype(ps)::value;             /* t % KT_PF */
         constexpr uint32_t CS = PS % KT_CL;                      /* C1 -> C2 set of this step */
         /* CLAMP: the step's loads may reach past the value (its last
          * blocks); otherwise they are plain 8-byte loads */
-        constexpr bool CLAMP = SMALL || decltype(clamp)::value != 0u;
+        constexpr bool CLAMP = SMALL || decltype(clamp)::value == 1u;
+        /* INTERIOR (clamp 2, KT_INTERIOR): t >= KT_PF and blocks t-3 .. t +
+         * KT_PF + 3 lie inside the value, so every block and position test
+         * of the step holds; they are dropped (no exec-mask branches) */
+        constexpr bool INTERIOR = !SMALL && decltype(clamp)::value == 2u;
+        const uint32_t m3_1 = m3 == 0u ? 2u : m3 - 1u;          /* (t - 1) % 3 */
+        const uint32_t m3_2 = m3 == 2u ? 0u : m3 + 1u;          /* (t - 2) % 3 */
         const auto ld8 = [&](uint32_t pp) { return CLAMP ? kt_ld8<SMALL>(src, n, pp) : dv_ld8(src + pp); };
         KT_T0();
+#ifdef KT_TIMING
+        const uint64_t kt_s = kt_t;
+#endif
         /* this step's global loads are issued unconditionally, by every
          * wave, at the end: a load inside a branch leaves a register merge
          * behind that waits for it */
@@ -221,10 +271,10 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
             /* ---- B(t-1): the table wave ------------------------------------- */
             /* one lane-ordered exchange per window, in window (= position)
              * order, five windows per asm group; no exec masking */
-            if (t >= 1u && t <= nb) {
+            if (INTERIOR || (t >= 1u && t <= nb)) {
                 const uint32_t k = t - 1u, B = KT_BLK * k;
                 const uint32_t *Sk = S + KT_BLK * (k & 1u);
-                uint16_t *Ok = O + KT_BLK * (k % 3u);
+                uint16_t *Ok = O + KT_BLK * m3_1;
                 /* a position past the value exchanges in its lane's own
                  * dummy half (T[65536 + lane]) */
                 const uint32_t tb = kt_lds_addr(T);
@@ -235,9 +285,17 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                     for (uint32_t u = 0; u < 5u; u++) {
                         const uint32_t i = g + u;
                         const uint32_t e = Sk[64u * i + lane];
+#if KT_SPRE
+                        /* the worker stored the exchange's dword address and
+                         * the slot's half (bit 0) */
+                        (void)tb;
+                        xs[u] = (e & 1u) << 4;
+                        xa[u] = e & ~3u;
+#else
                         const uint32_t h = (e & KS_ACT) ? (e & 0xFFFFu) : LZF_SLOTS + lane;
                         xs[u] = (h & 1u) << 4;
                         xa[u] = tb + 4u * (h >> 1);
+#endif
                         xm[u] = 0xFFFFu << xs[u];
                         xd[u] = ((B + 64u * i + lane) & 0xFFFFu) << xs[u];
                     }
@@ -248,7 +306,7 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
             }
         } else {
             /* ---- C2(t-2-KT_CL): agreement and record ------------------------ */
-            if (c_p[CS] < np) {
+            if (INTERIOR || c_p[CS] < np) {
                 const uint32_t cp = c_p[CS], cq1 = c_q1[CS], cq2 = c_q2[CS], cav = c_avail[CS];
                 const uint2 ca = c_a[CS], cb1 = c_b1[CS], cb2 = c_b2[CS];
                 /* branch-free: both agreements always, the record by selects */
@@ -261,25 +319,25 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 rec[cp] = cq1 ? (r1 | (cq2 ? r2 : 0u)) : 0u;
             }
             /* ---- Q <- O of block t-3 ---------------------------------------- */
-            if (t >= 3u && t - 3u < nb) {
+            if (INTERIOR || (t >= 3u && t - 3u < nb)) {
                 const uint32_t k = t - 3u;
                 const uint32_t x = KT_BLK * k + 64u * j + lane;
-                if (x < np) Q[x & (LZF_WINDOW - 1u)] = O[KT_BLK * (k % 3u) + 64u * j + lane];
+                if (INTERIOR || x < np) Q[x & (LZF_WINDOW - 1u)] = O[KT_BLK * m3 + 64u * j + lane];
             }
             KT_TM(2);
             /* ---- C1(t-2): q1, q2; their agreement loads below ---------------- */
             c_p[CS] = 0xFFFFFFFFu;
             c_q1[CS] = c_q2[CS] = 0u;
-            if (t >= 2u && t - 2u < nb) {
+            if (INTERIOR || (t >= 2u && t - 2u < nb)) {
                 const uint32_t k = t - 2u, B = KT_BLK * k;
                 const uint32_t p = B + 64u * j + lane;
                 /* branch-free: the Q..O read at a clamped index for every lane,
                  * validity by selects */
-                const bool act = p < np;
-                const uint16_t *Ok = O + KT_BLK * (k % 3u);
+                const bool act = INTERIOR || p < np;
+                const uint16_t *Ok = O + KT_BLK * m3_2;
                 const uint32_t q1r = Ok[64u * j + lane];
                 const uint32_t q1 = act && p - q1r <= LZF_WINDOW ? q1r : 0u;   /* q1r = 0: none */
-                const uint32_t ik = LZF_WINDOW + KT_BLK * (k % 3u), ip = LZF_WINDOW + KT_BLK * ((k + 2u) % 3u);
+                const uint32_t ik = LZF_WINDOW + KT_BLK * m3_2, ip = LZF_WINDOW + KT_BLK * m3;   /* (k + 2) % 3 = t % 3 */
                 const uint32_t iq = q1 >= B ? ik + (q1 - B)
                                   : q1 + KT_BLK >= B ? ip + (q1 + KT_BLK - B)
                                                      : (q1 & (LZF_WINDOW - 1u));
@@ -293,13 +351,24 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
             }
             KT_TM(3);
             /* ---- A(t): the worker's window of block t ----------------------- */
-            if (t < nb) {
+            if (INTERIOR || t < nb) {
                 const uint32_t p = KT_BLK * t + 64u * j + lane;
-                const bool act = p < np;
+                const bool act = INTERIOR || p < np;
                 const uint2 a = pf[PS];
                 ak[PS] = a;
                 const uint32_t s = dv_slot(a.x);
+#if KT_SPRE
+                {
+                    /* the table wave's exchange address (T's dword of the slot,
+                     * or the lane's dummy past the value) and half, so it does
+                     * not compute them: it shares its SIMD with three workers
+                     * and sets the step's pace there (tools/kt_trace.py) */
+                    const uint32_t h = act ? s : LZF_SLOTS + lane;
+                    S[KT_BLK * (t & 1u) + 64u * j + lane] = kt_lds_addr(T) + 4u * (h >> 1) + (h & 1u);
+                }
+#else
                 S[KT_BLK * (t & 1u) + 64u * j + lane] = act ? (s | KS_ACT) : 0u;
+#endif
             }
         }
         if (w) KT_TM(4);
@@ -310,35 +379,85 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
         c_b2[CS] = ld8(l2);
         pf[PS] = ld8(lp);
         if (w) KT_TM(5);
+#if defined(KT_TIMING) && defined(KT_LITE)
+        if (lane == 0u && blockIdx.x < KT_LW && kt_loc[7] < KT_LS)
+            kt_trace[(blockIdx.x * KT_LS + (uint32_t)kt_loc[7]) * 16u + w] =
+                (uint32_t)(__builtin_amdgcn_s_memtime() - kt_s);
+#elif defined(KT_TIMING)
+        /* each wave's busy cycles this step; after the barrier the table wave
+         * sums the slowest worker's (kt_acc[8]) and the mean worker's (9) */
+        if (lane == 0u) kt_busy[16u * (t & 1u) + w] = (uint32_t)(kt_t - kt_s);
+#endif
         __syncthreads();
         if (w) KT_TM(6);
         else KT_TM(1);
 #ifdef KT_TIMING
-        kt_acc[7]++;
+        kt_loc[7]++;
+#ifndef KT_LITE
+        if (w == 0u && lane == 0u) {
+            uint32_t mx = 0u, sm = 0u;
+            for (uint32_t i = 1; i <= KT_WIN; i++) {
+                const uint32_t b = kt_busy[16u * (t & 1u) + i];
+                mx = b > mx ? b : mx;
+                sm += b;
+            }
+            kt_loc[8] += mx;
+            kt_loc[9] += sm / KT_WIN;
+        }
+#endif
 #endif
     };
     /* steps whose loads all stay inside the value -- the input of block
      * t + KT_PF and agreement bytes of positions before block t - 1 -- skip
      * the end-of-value clamp (the last group of steps keeps it) */
-    uint32_t t = 0;
-    if (!SMALL)
-        for (; t < nb + 2u + KT_CL && KT_BLK * (t + 3u + KT_PF + 1u) + 8u <= n; t += KT_PF) {
-            step(KtIc<0>{}, KtIc<0>{}, t);
-            step(KtIc<1>{}, KtIc<0>{}, t + 1u);
-            step(KtIc<2>{}, KtIc<0>{}, t + 2u);
-            step(KtIc<3>{}, KtIc<0>{}, t + 3u);
+    uint32_t t = 0, m3 = 0;                                    /* m3 = t % 3 */
+    const auto next3 = [](uint32_t x) { return x == 2u ? 0u : x + 1u; };
+    if (!SMALL) {
+        if (KT_INTERIOR && KT_BLK * (KT_PF + 3u + KT_PF + 1u) + 8u <= n) {
+            /* the first KT_PF steps test their blocks (t - 3 < 0 ...) */
+            step(KtIc<0>{}, KtIc<0>{}, 0u, 0u);
+            step(KtIc<1>{}, KtIc<0>{}, 1u, 1u);
+            step(KtIc<2>{}, KtIc<0>{}, 2u, 2u);
+            step(KtIc<3>{}, KtIc<0>{}, 3u, 0u);
+            t = KT_PF;
+            m3 = KT_PF % 3u;
+            for (; t < nb + 2u + KT_CL && KT_BLK * (t + 3u + KT_PF + 1u) + 8u <= n; t += KT_PF) {
+                step(KtIc<0>{}, KtIc<2>{}, t, m3);
+                m3 = next3(m3);
+                step(KtIc<1>{}, KtIc<2>{}, t + 1u, m3);
+                m3 = next3(m3);
+                step(KtIc<2>{}, KtIc<2>{}, t + 2u, m3);
+                m3 = next3(m3);
+                step(KtIc<3>{}, KtIc<2>{}, t + 3u, m3);
+                m3 = next3(m3);
+            }
         }
+        for (; t < nb + 2u + KT_CL && KT_BLK * (t + 3u + KT_PF + 1u) + 8u <= n; t += KT_PF) {
+            step(KtIc<0>{}, KtIc<0>{}, t, m3);
+            m3 = next3(m3);
+            step(KtIc<1>{}, KtIc<0>{}, t + 1u, m3);
+            m3 = next3(m3);
+            step(KtIc<2>{}, KtIc<0>{}, t + 2u, m3);
+            m3 = next3(m3);
+            step(KtIc<3>{}, KtIc<0>{}, t + 3u, m3);
+            m3 = next3(m3);
+        }
+    }
     /* (a per-step tail, to run no empty steps past the last, measured
      * slower: its switch costs more than the steps it saves) */
     for (; t < nb + 2u + KT_CL; t += KT_PF) {
-        step(KtIc<0>{}, KtIc<1>{}, t);
-        step(KtIc<1>{}, KtIc<1>{}, t + 1u);
-        step(KtIc<2>{}, KtIc<1>{}, t + 2u);
-        step(KtIc<3>{}, KtIc<1>{}, t + 3u);
+        step(KtIc<0>{}, KtIc<1>{}, t, m3);
+        m3 = next3(m3);
+        step(KtIc<1>{}, KtIc<1>{}, t + 1u, m3);
+        m3 = next3(m3);
+        step(KtIc<2>{}, KtIc<1>{}, t + 2u, m3);
+        m3 = next3(m3);
+        step(KtIc<3>{}, KtIc<1>{}, t + 3u, m3);
+        m3 = next3(m3);
     }
 #ifdef KT_TIMING
-    if (lane == 0u)
-        for (uint32_t i = 0; i < 8u; i++) atomicAdd(&kt_times[i], (unsigned long long)kt_acc[i]);
+#pragma unroll
+    for (uint32_t i = 0; i < 10u; i++) kt_acc[i] += kt_loc[i];
 #endif
 }
 
@@ -351,8 +470,23 @@ __global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt,
     uint16_t *const Q = QO, *const O = QO + LZF_WINDOW;
     __shared__ uint32_t S[2u * KT_BLK];
     const KtLds L{T, Q, O, S};
+#ifdef KT_PMAP
+    {
+        /* per-wave issue priority, 2 bits per wave index (experiment) */
+        const uint32_t pw = (uint32_t)((KT_PMAP >> (4u * (threadIdx.x >> 6))) & 3u);
+        if (pw == 1u) __builtin_amdgcn_s_setprio(1);
+        else if (pw == 2u) __builtin_amdgcn_s_setprio(2);
+        else if (pw == 3u) __builtin_amdgcn_s_setprio(3);
+    }
+#endif
 #ifdef KT_PRIO
     if (threadIdx.x < 64u) __builtin_amdgcn_s_setprio(KT_PRIO);   /* the table wave */
+#endif
+#ifdef KT_TIMING
+    /* summed per wave over its values, added once at the end (per-value
+     * atomics on one line serialised and skewed the timings) */
+    uint64_t kt_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    __shared__ uint32_t kt_busy[32];
 #endif
     for (uint32_t v = blockIdx.x; v < bt.count; v += gridDim.x) {
         const uint32_t n = bt.in_len[v];
@@ -361,9 +495,13 @@ __global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt,
         if (n < 3u || n > LZF_SLOTS || n > bt.max_len) continue;
         const uint8_t *src = bt.in + bt.in_off[v];
         uint32_t *rec = sc.rec + (uint64_t)v * sc.rstride;
-        if (n >= 8u) kt_value<false>(L, src, n, rec);
-        else kt_value<true>(L, src, n, rec);
+        if (n >= 8u) kt_value<false>(L, src, n, rec KT_ACC_PASS);
+        else kt_value<true>(L, src, n, rec KT_ACC_PASS);
     }
+#ifdef KT_TIMING
+    if ((threadIdx.x & 63u) == 0u)
+        for (uint32_t i = 0; i < 10u; i++) atomicAdd(&kt_times[i], (unsigned long long)kt_acc[i]);
+#endif
 }
 
 /* ======================================================================== */

@@ -18,6 +18,7 @@
 #   env:K:N:C:S[:S..]   compress A/B of env settings (tools/ab_env.py; a setting uses , and =)
 #   tstat:K:N:C         the pipe decoder's phase cycles (CD_TIMING build liblzf_hip_time.so)
 #   kt:K:N:C:LIB        per-phase cycles of the table cand kernel (-DKT_TIMING build liblzf_hip_LIB.so)
+#   ktr:K:N:C           per-step busy cycles of every cand wave (tools/kt_trace.py, liblzf_hip_ktlite.so)
 #   k3:K:N:C:LIB        per-value counters of the record parse (-DKT_TIMING build liblzf_hip_LIB.so)
 #   xo:K:N:C:COUNTS     routed generation vs window64 by batch size (tools/crossover.py)
 #   host[:reg]          PCIe-inclusive host-path rates (tools/host_path_bench.py); :reg registered only
@@ -92,6 +93,11 @@ for st in "$@"; do
       IFS=: read -r _ k nn c lib <<< "$st"
       LZF_HIP_LIB=$PWD/gibson_amd/liblzf_hip_$lib.so timeout -k 10 300 python -u tools/kt_timing.py $k $nn $c > $O/kt_${lib}_${k}_${nn}.txt 2>&1 || exit 1
       quiet $O/kt_${lib}_${k}_${nn}.txt ;;
+    ktr:*)
+      # ktr:K:N:C -- per-step busy cycles of every cand wave (-DKT_TIMING -DKT_LITE build liblzf_hip_ktlite.so)
+      IFS=: read -r _ k nn c <<< "$st"
+      timeout -k 10 300 python -u tools/kt_trace.py $k $nn $c > $O/ktr_${k}_${nn}.txt 2>&1 || exit 1
+      quiet $O/ktr_${k}_${nn}.txt ;;
     k3:*)
       # k3:K:N:C:LIB -- per-value counters of the record parse (a -DKT_TIMING build gibson_amd/liblzf_hip_LIB.so)
       IFS=: read -r _ k nn c lib <<< "$st"

@@ -43,3 +43,5 @@ print(f"kernel {e0.elapsed_time(e1):.2f} ms, {steps:.0f} workgroup-steps")
 for i, nm in enumerate(names):
     per = v[i] / steps / (1 if i < 2 else nw)
     print(f"  {nm:22s} {per:9.1f} cycles per step (per wave)")
+if v[8]:   # busy cycles before the barrier: the slowest worker and the mean worker, per step
+    print(f"  workers' busy time per step: slowest {v[8] / steps:9.1f}, mean {v[9] / steps:9.1f} cycles")
