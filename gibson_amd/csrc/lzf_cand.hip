@@ -65,6 +65,14 @@
 #define KT_CL 2u                /* steps from C1 (agreement loads issued) to C2 (consumed); divides KT_PF */
 #endif
 
+/* v_ffbl_b32: the lowest set bit's index, 0xFFFFFFFF for 0 (defined here,
+ * unlike __builtin_ctz) */
+__device__ __forceinline__ uint32_t kt_ffbl(uint32_t x)
+{
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
 __device__ __forceinline__ uint32_t kt_code(uint32_t k)
 {
     return k < 3u ? RC_DIFF : (k >= 8u ? RC_LONG : k - 1u);
@@ -180,6 +188,13 @@ template <uint32_t V> struct KtIc { static constexpr uint32_t value = V; };
 /* KT_SPRE (round 5): workers store the table wave's exchange address */
 #ifndef KT_SPRE
 #define KT_SPRE 1
+#endif
+/* round 5: C2's agreements without 64-bit compares, C1's q2 index by selects */
+#ifndef KT_AGREE2
+#define KT_AGREE2 1
+#endif
+#ifndef KT_IQSEL
+#define KT_IQSEL 1
 #endif
 
 #ifdef KT_TIMING
@@ -297,7 +312,7 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                         xa[u] = tb + 4u * (h >> 1);
 #endif
                         xm[u] = 0xFFFFu << xs[u];
-                        xd[u] = ((B + 64u * i + lane) & 0xFFFFu) << xs[u];
+                        xd[u] = (((B + 64u * i) & 0xFFFFu) | lane) << xs[u];   /* B + 64 i: a multiple of 64 */
                     }
                     kt_xchg5(xr, xa, xm, xd);
 #pragma unroll
@@ -312,8 +327,16 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 /* branch-free: both agreements always, the record by selects */
                 const uint64_t x1 = ((uint64_t)(ca.y ^ cb1.y) << 32) | (uint64_t)(ca.x ^ cb1.x);
                 const uint64_t x2 = ((uint64_t)(ca.y ^ cb2.y) << 32) | (uint64_t)(ca.x ^ cb2.x);
+#if KT_AGREE2
+                /* first differing byte of 8 (8: none), without the 64-bit compare
+                 * and select: v_ffbl gives the lowest set bit or ~0 for none, so
+                 * min3(ffbl(lo), ffbl(hi) | 32, 64) is the first differing bit */
+                const uint32_t k1 = min(min(min(kt_ffbl((uint32_t)x1), kt_ffbl((uint32_t)(x1 >> 32)) | 32u), 64u) >> 3, cav);
+                const uint32_t k2 = min(min(min(kt_ffbl((uint32_t)x2), kt_ffbl((uint32_t)(x2 >> 32)) | 32u), 64u) >> 3, cav);
+#else
                 const uint32_t k1 = min(x1 ? (uint32_t)__builtin_ctzll(x1) >> 3 : 8u, cav);
                 const uint32_t k2 = min(x2 ? (uint32_t)__builtin_ctzll(x2) >> 3 : 8u, cav);
+#endif
                 const uint32_t r1 = (cp - cq1 - 1u) | (kt_code(k1) << 13);
                 const uint32_t r2 = ((cp - cq2 - 1u) | (kt_code(k2) << 13)) << 16;
                 rec[cp] = cq1 ? (r1 | (cq2 ? r2 : 0u)) : 0u;
@@ -338,9 +361,17 @@ __device__ __forceinline__ void kt_value(const KtLds &L, const uint8_t *src, uin
                 const uint32_t q1r = Ok[64u * j + lane];
                 const uint32_t q1 = act && p - q1r <= LZF_WINDOW ? q1r : 0u;   /* q1r = 0: none */
                 const uint32_t ik = LZF_WINDOW + KT_BLK * m3_2, ip = LZF_WINDOW + KT_BLK * m3;   /* (k + 2) % 3 = t % 3 */
+#if KT_IQSEL
+                /* all three indices, then selects (the nested ternary compiled to
+                 * exec-mask branches: ~20 SALU per step) */
+                const uint32_t iq0 = ik + (q1 - B), iq1 = ip + (q1 + KT_BLK - B), iq2 = q1 & (LZF_WINDOW - 1u);
+                const uint32_t iq01 = q1 + KT_BLK >= B ? iq1 : iq2;
+                const uint32_t iq = q1 >= B ? iq0 : iq01;
+#else
                 const uint32_t iq = q1 >= B ? ik + (q1 - B)
                                   : q1 + KT_BLK >= B ? ip + (q1 + KT_BLK - B)
                                                      : (q1 & (LZF_WINDOW - 1u));
+#endif
                 const uint32_t q2r = Q[iq];
                 const uint32_t q2 = q1 && q2r != 0u && p - q2r <= LZF_WINDOW ? q2r : 0u;
                 c_p[CS] = act ? p : 0xFFFFFFFFu;
