@@ -158,10 +158,23 @@ extern "C" int lzf_gpu_debug_ks(unsigned long long *out16, int reset)
 __device__ __forceinline__ uint32_t ks_code(uint32_t k) { return k < 3u ? 1u : (k >= 8u ? 7u : k - 1u); }
 
 /* agreement of 8 bytes a (at p) and b (at q), at most avail = n - p */
+#ifndef KS_FFBL
+#define KS_FFBL 1
+#endif
 __device__ __forceinline__ uint32_t ks_agree(uint2 a, uint2 b, uint32_t avail)
 {
+#if KS_FFBL
+    /* v_ffbl gives the lowest set bit or ~0 for none: min3(ffbl(lo),
+     * ffbl(hi) | 32, 64) is the first differing bit, 64 for none (round 5:
+     * no 64-bit compare and select) */
+    uint32_t fl, fh;
+    asm("v_ffbl_b32 %0, %1" : "=v"(fl) : "v"(a.x ^ b.x));
+    asm("v_ffbl_b32 %0, %1" : "=v"(fh) : "v"(a.y ^ b.y));
+    const uint32_t k = min(min(fl, fh | 32u), 64u) >> 3;
+#else
     const uint64_t x = ((uint64_t)(a.y ^ b.y) << 32) | (uint64_t)(a.x ^ b.x);
     const uint32_t k = x ? (uint32_t)__builtin_ctzll(x) >> 3 : 8u;
+#endif
     return k < avail ? k : avail;
 }
 
