@@ -195,6 +195,10 @@ __device__ __forceinline__ void cd_stage(uint8_t *inr, const uint8_t *src, uint3
 #ifndef CD_PREF2
 #define CD_PREF2 1
 #endif
+/* tokpar64: the next staging piece prefetched into registers (round 5) */
+#ifndef CD_TPREF
+#define CD_TPREF 1
+#endif
 template <uint32_t V> struct CdPar { static constexpr uint32_t value = V; };
 __device__ uint4 cd_dummy16;    /* the idle lanes' load address */
 /* CD_CPRIO: issue priority of the pipe's consumer wave (s_setprio).  VALU
@@ -540,9 +544,44 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
     uint32_t F = 0;             /* output [0, F) stored */
     int32_t err = 0;
     bool first = true;
+    /* CD_TPREF: the next staging piece in registers, loaded when the one
+     * before it is written (one 16-byte load per lane, the stream's last piece
+     * from avail - 16, idle lanes from a dummy: no byte loop, no branch), so a
+     * staging waits for no load (streams of < 16 bytes stage synchronously) */
+    uint4 pv = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t pf = 0u, pt = 0u;                        /* pv holds [pf, pt) */
     while (first || base < in_len) {                     /* src/lzf_d.c:64, 146 */
         first = false;
-        cd_stage<CD_IN_RING1>(inr, src, base, avail, loaded, lane);
+        if (CD_TPREF && avail >= 16u) {
+            constexpr uint32_t STAGE = CD_IN_RING1 / 2u;
+            uint32_t need = base + 2u * CD_ROUND;
+            if (need > avail) need = avail;
+            if (loaded < need) {
+                const uint32_t to = min(loaded + STAGE, avail);
+                const uint32_t x = loaded + 16u * lane;
+                if (pt > pf) {                       /* the prefetched piece: [loaded, to) */
+                    if (x < pt) {
+                        const uint32_t d = pt - x < 16u ? 16u - (pt - x) : 0u;
+                        uint4 w = pv;
+                        if (d) w = cd_shr16(w, d);
+                        *(uint4 *)(inr + (x & (CD_IN_RING1 - 1u))) = w;
+                    }
+                } else if (x < to) {
+                    *(uint4 *)(inr + (x & (CD_IN_RING1 - 1u))) = cd_ld16(src + x, to - x);
+                }
+                loaded = to;
+                cd_fence();
+                /* the piece after it */
+                const uint32_t to2 = min(loaded + STAGE, avail);
+                const uint32_t x2 = loaded + 16u * lane;
+                const uint8_t *pa = x2 < to2 ? src + (to2 - x2 >= 16u ? x2 : avail - 16u) : (const uint8_t *)&cd_dummy16;
+                __builtin_memcpy(&pv, pa, 16);
+                pf = loaded;
+                pt = to2;
+            }
+        } else {
+            cd_stage<CD_IN_RING1>(inr, src, base, avail, loaded, lane);
+        }
         const uint32_t x = cd_discover_lds<TSZT>(inr, imask, jt, base, in_len, lane);
         const CdRound r = cd_decode(inr, imask, base, x, O, in_len, cap);
         if (r.err) {
