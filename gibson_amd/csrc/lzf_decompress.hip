@@ -487,6 +487,46 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
  * The 16-bit start marks of tokpar64's windows of <= 4 KiB rely on this:
  * with out_cap <= max_len <= the window, a stream's output positions stay
  * below 65536, so a stale mark never matches a later group */
+/* a stream's fields, every load issued before any is used (CD_META, round
+ * 5: the skip flag, the refusal test and the offsets were four dependent
+ * memory waits before the first input load) */
+#ifndef CD_META
+#define CD_META 1
+#endif
+struct CdMeta {
+    uint32_t in_len, cap, max_len;
+    const uint8_t *src;
+    uint8_t *dst;
+    bool skip;
+};
+__device__ __forceinline__ CdMeta cd_meta(const LzfBatch &bt, uint32_t v)
+{
+    CdMeta m;
+    const uint8_t *sp = bt.skip ? bt.skip + v : (const uint8_t *)&cd_dummy16;   /* zero when there is no skip list */
+    m.in_len = __builtin_amdgcn_readfirstlane(bt.in_len[v]);
+    m.cap = __builtin_amdgcn_readfirstlane(bt.out_cap[v]);
+    const uint64_t io = bt.in_off[v], oo = bt.out_off[v];
+    const uint32_t sk = *sp;
+    m.max_len = bt.max_len;
+    /* all of them used here, before the skip and refusal branches: the
+     * compiler would otherwise sink loads past them (one more wait each) */
+    asm volatile("" ::"s"(io), "s"(oo), "v"(sk), "s"(m.max_len));
+    m.src = bt.in + io;
+    m.dst = bt.out + oo;
+    m.skip = __builtin_amdgcn_readfirstlane(sk) != 0u;
+    return m;
+}
+/* a value whose out_cap exceeds the batch's max_len is refused (EINVAL) */
+__device__ __forceinline__ bool cd_refuse_cap(const LzfBatch &bt, uint32_t v, uint32_t cap, uint32_t max_len,
+                                              uint32_t lane)
+{
+    if (cap <= max_len) return false;
+    if (lane == 0) {
+        bt.out_len[v] = 0u;
+        bt.err[v] = 22;             /* EINVAL */
+    }
+    return true;
+}
 __device__ __forceinline__ bool cd_refused(const LzfBatch &bt, uint32_t v, uint32_t lane)
 {
     if (bt.out_cap[v] <= bt.max_len) return false;
@@ -530,11 +570,20 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
 
     const uint32_t lane = threadIdx.x;
     const uint32_t v = blockIdx.x;
+#if CD_META
+    const CdMeta md = cd_meta(bt, v);
+    if (md.skip || cd_refuse_cap(bt, v, md.cap, md.max_len, lane)) return;
+    const uint32_t in_len = md.in_len;
+    const uint32_t cap = md.cap;
+    const uint8_t *src = md.src;
+    uint8_t *dst = md.dst;
+#else
     if ((bt.skip && bt.skip[v]) || cd_refused(bt, v, lane)) return;
     const uint32_t in_len = bt.in_len[v];
     const uint32_t cap = bt.out_cap[v];
     const uint8_t *src = bt.in + bt.in_off[v];
     uint8_t *dst = bt.out + bt.out_off[v];
+#endif
     /* as the reference, a 0-length stream still reads its first control byte */
     const uint32_t avail = in_len ? in_len : 1u;
 
@@ -647,9 +696,16 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
     const uint32_t lane = threadIdx.x & 63u;
     const bool producer = threadIdx.x < 64u;
     const uint32_t v = blockIdx.x;
+#if CD_META
+    const CdMeta md = cd_meta(bt, v);
+    if (md.skip || cd_refuse_cap(bt, v, md.cap, md.max_len, threadIdx.x)) return;
+    const uint32_t in_len = md.in_len;   /* scalar: no load wait in the loop */
+    const uint32_t cap = md.cap;
+#else
     if ((bt.skip && bt.skip[v]) || cd_refused(bt, v, threadIdx.x)) return;
     const uint32_t in_len = __builtin_amdgcn_readfirstlane(bt.in_len[v]);   /* scalar: no load wait in the loop */
     const uint32_t cap = __builtin_amdgcn_readfirstlane(bt.out_cap[v]);
+#endif
 
     uint64_t tw[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
 #ifdef CD_TIMING
@@ -658,7 +714,11 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
     if (producer) {
         /* steps 1-3, one round ahead of the consumer; round k's table goes to
          * slot k & 1, published by the barrier that ends round k */
+#if CD_META
+        const uint8_t *src = md.src;
+#else
         const uint8_t *src = bt.in + bt.in_off[v];
+#endif
         const uint32_t avail = in_len ? in_len : 1u;   /* a 0-length stream still reads one byte */
         uint32_t loaded = 0, base = 0, O = 0;
         cd_jt_init(jt, lane);
@@ -778,7 +838,11 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
             if (round(CdPar<1>(), k + 1u)) break;
         }
     } else {
+#if CD_META
+        uint8_t *dst = md.dst;
+#else
         uint8_t *dst = bt.out + bt.out_off[v];
+#endif
         if (CD_CPRIO) __builtin_amdgcn_s_setprio(CD_CPRIO);
         uint32_t O = 0, F = 0;  /* output [0, F) stored */
         int32_t err = 0;
