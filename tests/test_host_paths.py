@@ -268,3 +268,56 @@ def test_registered_tail_mode_64k(oracle, registered, monkeypatch, share, chunks
     for i in sorted(set(list(range(0, count, 97)) + [e + d for e in edges for d in (-1, 0)] + [count - 1])):
         exp = oracle.compress(bytes(arena[i * n:(i + 1) * n]), n - 4)
         assert bytes(out_r[i * n:i * n + olen_r[i]]) == exp, i
+
+
+@pytest.mark.parametrize("env", [{}, {"LZF_GPU_HOST_NCHUNKS": "1"}, {"LZF_GPU_HOST_TAIL": "0"},
+                                 {"LZF_GPU_HOST_TAIL_CHUNKS": "3", "LZF_GPU_HOST_TAIL": "40"}],
+                         ids=["default", "one-chunk", "tail-off", "tail40-3chunks"])
+def test_registered_bulk_mixed_sizes(oracle, registered, monkeypatch, env):
+    # a bulk compress batch (>= 192 MiB) of 0 B .. 64 KiB values at unaligned,
+    # shuffled arena offsets: the chunk plan, the tail mode and its window64
+    # part over ragged values, against the staged path and an oracle sample
+    # that includes every chunk's edges; then the round trip
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    import gibson_amd
+    rnd = random.Random(57)
+    count = 12288
+    sizes = [rnd.choice([65536, rnd.randint(0, 65536), rnd.randint(0, 20000)]) for _ in range(count)]
+    order = list(range(count))
+    rnd.shuffle(order)
+    pos, offs = 0, [0] * count
+    for i in order:
+        offs[i] = pos
+        pos += sizes[i] + rnd.randint(0, 5)
+    assert pos >= 192 << 20
+    arena = registered(_aligned(pos + 16))
+    for i in range(count):
+        arena[offs[i]:offs[i] + sizes[i]] = np.frombuffer(synth((2, 3, 1)[i % 3], 0x5EED00B5, i, sizes[i]), np.uint8)
+    off = np.array(offs, dtype=np.uint64)
+    ln = np.array(sizes, dtype=np.uint32)
+    cap = np.maximum(ln.astype(np.int64) - 4, 0).astype(np.uint32)
+    out_r = registered(_aligned(pos + 16))
+    olen_r = np.zeros(count, np.uint32)
+    gibson_amd.host_compress_batch(arena, off, ln, out_r, off, cap, olen_r)
+    out_s = np.zeros(pos + 16, np.uint8)
+    olen_s = np.zeros(count, np.uint32)
+    gibson_amd.host_compress_batch(arena, off, ln, out_s, off, cap, olen_s)
+    assert np.array_equal(olen_r, olen_s)
+    for i in range(count):
+        assert bytes(out_r[offs[i]:offs[i] + olen_r[i]]) == bytes(out_s[offs[i]:offs[i] + olen_s[i]]), i
+    edges = {0, count - 1} | {count * p // 100 + d for p in (40, 70) for d in (-1, 0)} | \
+        {count * k // 3 + d for k in (1, 2) for d in (-1, 0)}
+    for i in sorted(edges | set(rnd.sample(range(count), 150))):
+        v = bytes(arena[offs[i]:offs[i] + sizes[i]])
+        exp = oracle.compress(v, int(cap[i])) if sizes[i] and cap[i] else None
+        got = bytes(out_r[offs[i]:offs[i] + olen_r[i]]) if olen_r[i] else None
+        assert got == exp, i
+    ok = olen_r > 0
+    dec = registered(_aligned(pos + 16))
+    dl = np.zeros(int(ok.sum()), np.uint32)
+    er = np.zeros(int(ok.sum()), np.int32)
+    gibson_amd.host_decompress_batch(out_r, off[ok], olen_r[ok], dec, off[ok], ln[ok], dl, er)
+    assert (dl == ln[ok]).all() and (er == 0).all()
+    for i in np.nonzero(ok)[0]:
+        assert bytes(dec[offs[i]:offs[i] + sizes[i]]) == bytes(arena[offs[i]:offs[i] + sizes[i]]), i
