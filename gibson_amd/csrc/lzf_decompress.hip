@@ -371,7 +371,13 @@ __device__ __forceinline__ void cd_flush(const uint8_t *lds, uint32_t outr_off, 
 #ifndef CD_MARKAHEAD_PIPE           /* the pipe's consumer */
 #define CD_MARKAHEAD_PIPE 0
 #endif
-template <uint32_t IN_RING, bool PER = false, bool MA = CD_MARKAHEAD, typename MT = uint32_t>
+/* FAR (round 5): the window is a ring smaller than the 8 KiB that
+ * back-references reach (src/lzf_d.c:95); a source more than a window behind
+ * the group is read back from the output in HBM, where the flush put it (the
+ * flush lags the group by at most a unit + 64 bytes, less than a window; a
+ * workgroup-scope release after each flush makes the stores visible to the
+ * wave's own later loads) */
+template <uint32_t IN_RING, bool PER = false, bool MA = CD_MARKAHEAD, typename MT = uint32_t, bool FAR = false>
 __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint32_t omask, MT *mark,
                                              uint32_t sink_off, uint8_t *dst, uint32_t O, uint32_t total, bool tok,
                                              uint32_t Ot, uint32_t tinfo, uint32_t lane, uint32_t &F)
@@ -439,7 +445,14 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
         const uint32_t li = IN_RING <= omask + 1u ? (so & imask) | (omask + 1u) : (so & imask) + (omask + 1u);
         const uint32_t a = outr_off + (lit ? li : so & omask);
         const uint32_t q = so - gb;
-        const uint32_t b = lds[a];
+        uint32_t b = lds[a];
+        if (FAR) {
+            /* a source more than a window behind the group's start: out of the ring */
+            const bool far = !lit && so < gb && gb - so > omask + 1u;
+            if (cd_ballot(far)) {
+                if (far) b = dst[so];
+            }
+        }
         /* resolved: bit 31 | the byte; pending: the source lane's ds_bpermute
          * address (lane × 4) in bits 10-15 */
         const bool pend = !lit && q < CD_LANES;
@@ -464,6 +477,7 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
                     __builtin_memcpy(dst + x, &v, 16);
                 }
                 F += unit;
+                if (FAR) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             }
         }
     }
@@ -551,7 +565,7 @@ __device__ __forceinline__ bool cd_refused(const LzfBatch &bt, uint32_t v, uint3
 template <bool B> struct CdMark { typedef uint32_t T; };
 template <> struct CdMark<true> { typedef uint16_t T; };
 /* one instance per window size, with static LDS (as the pipe) */
-template <uint32_t RING>
+template <uint32_t RING, bool FAR = false>
 __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, uint32_t out_ring)
 {
     constexpr bool SMALL = CD_TP_SMALL && RING <= 4096u;
@@ -637,7 +651,7 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
             err = r.err;
             break;
         }
-        cd_output<CD_IN_RING1, false, CD_MARKAHEAD, MT>(smem, 0u, omask, mark, (uint32_t)(sink - smem), dst, O, r.total,
+        cd_output<CD_IN_RING1, false, CD_MARKAHEAD, MT, FAR>(smem, 0u, omask, mark, (uint32_t)(sink - smem), dst, O, r.total,
                                x < CD_ROUND, O + r.rel, r.tinfo, lane, F);
         O += r.total;
         base = r.nbase;
@@ -900,10 +914,21 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
 #define CD_PIPE_MIN_RING 8192u
 #endif
 
+/* CD_FAR_MAX (round 5, experiment): values over 4 KiB and up to this size
+ * decode with tokpar64's 4 KiB window (16-bit marks: outputs < 65536) and far
+ * sources read back from HBM, one wave per stream (32 streams per CU), instead
+ * of the pipe (0: off) */
+#ifndef CD_FAR_MAX
+#define CD_FAR_MAX 16384u
+#endif
 hipError_t lzf_launch_decompress(const LzfBatch &b, hipStream_t s)
 {
     uint32_t ring = 256u;
     while (ring < b.max_len && ring < CD_OUT_MAX) ring <<= 1;
+    if (CD_FAR_MAX && b.max_len > 4096u && b.max_len <= CD_FAR_MAX && b.max_len <= 65536u) {
+        hipLaunchKernelGGL((lzf_decompress_tokpar_kernel<4096u, true>), dim3(b.count), dim3(CD_LANES), 0, s, b, 4096u);
+        return hipGetLastError();
+    }
     if (CD_PIPE && ring >= CD_PIPE_MIN_RING) {
         if (ring != CD_OUT_MAX) return hipErrorInvalidValue;   /* static LDS for the 8 KiB window */
         hipLaunchKernelGGL(lzf_decompress_pipe_kernel, dim3(b.count), dim3(2u * CD_LANES), 0, s, b, ring);
@@ -941,4 +966,10 @@ extern "C" int lzf_gpu_dec_tstat(unsigned long long *out)
 }
 #endif
 
-const char *lzf_decompress_kernel_name(void) { return CD_PIPE ? "pipe" : "tokpar64"; }
+const char *lzf_decompress_kernel_name(void)
+{
+    if (!CD_PIPE) return "tokpar64";
+    return CD_FAR_MAX ? (CD_FAR_MAX >= 16384u ? "tokpar64 up to 4 KiB, tokpar64-far up to 16 KiB, pipe past"
+                                              : "tokpar64 up to 4 KiB, tokpar64-far up to 8 KiB, pipe past")
+                      : "tokpar64 up to 4 KiB, pipe past";
+}

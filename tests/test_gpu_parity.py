@@ -724,3 +724,46 @@ def test_decode_self_overlapping_references(oracle):
     streams = [oracle.compress(v, len(v) + len(v) // 16 + 64) for v in vals]
     assert all(streams)
     assert gpu_decompress(streams, [len(v) for v in vals]) == [(v, 0) for v in vals]
+
+
+@pytest.mark.parametrize("nmax", [8192, 16384, 16385])
+def test_decode_far_sources(oracle, nmax):
+    # batches whose largest value is 4-16 KiB decode on the 4 KiB tokpar
+    # window with sources more than 4 KiB behind the output group read back
+    # from dst in HBM (CD_FAR_MAX); 16385 takes the 8 KiB pipe instead.  A
+    # random block repeated at distances 4095..8192 (the LZF maximum, src/
+    # lzf_d.c:121) puts copies on both sides of the window edge, self-
+    # overlapping runs straddle it, and values at the batch maximum share the
+    # launch with tiny ones
+    from tests.gpu_batch import gpu_decompress
+    rnd = random.Random(nmax)
+    vals = []
+    for dist in (4095, 4096, 4097, 4100, 4160, 5000, 6144, 8000, 8191, 8192):
+        for phase in (0, 5, 63):
+            blk = bytes(rnd.randrange(256) for _ in range(dist))
+            v = bytes(rnd.randrange(256) for _ in range(phase)) + blk
+            while len(v) < nmax:
+                v += blk[:rnd.randint(3, 300)] + bytes(rnd.randrange(256) for _ in range(rnd.randint(0, 40)))
+            vals.append(v[:nmax - rnd.randrange(0, 64)])
+    for period in (1, 2, 7, 64, 65):
+        head = bytes(rnd.randrange(256) for _ in range(4090))
+        pat = bytes(rnd.randrange(256) for _ in range(period))
+        vals.append((head + pat * (nmax // period + 1))[:nmax])
+    vals += [b"", b"a", synth(0, 0xFA2, 1, 300), synth(1, 0xFA2, 2, nmax)]
+    vals.append(vals[0][:nmax])
+    streams = [oracle.compress(v, len(v) + len(v) // 16 + 64) if v else b"" for v in vals]
+    assert all(s or not v for s, v in zip(streams, vals))
+    keep = [i for i, v in enumerate(vals) if v]
+    got = gpu_decompress([streams[i] for i in keep], [len(vals[i]) for i in keep])
+    assert got == [(vals[i], 0) for i in keep]
+    # the same streams truncated: the errno the reference returns on the
+    # FAR route's batches (src/lzf_d.c:79-82, 110-114, 127-130)
+    bad_s, bad_l = [], []
+    for i in keep[:12]:
+        s = streams[i]
+        bad_s.append(s[:len(s) * 2 // 3])
+        bad_l.append(len(vals[i]))
+    res = gpu_decompress(bad_s, bad_l)
+    for s, n, (out, e) in zip(bad_s, bad_l, res):
+        ref = oracle.decompress(s, n)
+        assert (out, e) == ref
