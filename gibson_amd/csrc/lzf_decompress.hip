@@ -368,6 +368,9 @@ __device__ __forceinline__ void cd_flush(const uint8_t *lds, uint32_t outr_off, 
 #ifndef CD_MARKAHEAD
 #define CD_MARKAHEAD 1
 #endif
+#ifndef CD_FAR2                     /* FAR's one-compare test, its wait on its own path */
+#define CD_FAR2 1
+#endif
 #ifndef CD_MARKAHEAD_PIPE           /* the pipe's consumer */
 #define CD_MARKAHEAD_PIPE 0
 #endif
@@ -393,6 +396,7 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
 #endif
     /* lanes without a token mark slot 64 (never read): their start lies 2^31 away */
     const uint32_t Otm = tok ? Ot : Ot + 0x80000000u;
+    const uint32_t farb = 0u - (lane + omask + 2u);   /* FAR: tInf - lane - (window + 1) */
     /* a start mark holds the token's own start, so it matches only in its
      * group (no per-group tag; position 0, the unwritten marks' 0, always
      * starts a token) */
@@ -448,10 +452,23 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
         uint32_t b = lds[a];
         if (FAR) {
             /* a source more than a window behind the group's start: out of the ring */
+#if CD_FAR2
+            /* gb - so = tInf - lane for a back-reference (a periodic source
+             * only exists for distances < 264); literals carry bit 31 and
+             * in-group sources wrap, so one add and one compare decide it.
+             * The load's wait stays on this path: a wait after the join
+             * would hold every group for the flush's outstanding stores */
+            const bool far = tInf + farb < 8191u - omask;
+            if (far) {
+                b = dst[so];
+                asm volatile("" ::"v"(b));
+            }
+#else
             const bool far = !lit && so < gb && gb - so > omask + 1u;
             if (cd_ballot(far)) {
                 if (far) b = dst[so];
             }
+#endif
         }
         /* resolved: bit 31 | the byte; pending: the source lane's ds_bpermute
          * address (lane × 4) in bits 10-15 */
@@ -914,10 +931,11 @@ __global__ __launch_bounds__(128) void lzf_decompress_pipe_kernel(LzfBatch bt, u
 #define CD_PIPE_MIN_RING 8192u
 #endif
 
-/* CD_FAR_MAX (round 5, experiment): values over 4 KiB and up to this size
- * decode with tokpar64's 4 KiB window (16-bit marks: outputs < 65536) and far
- * sources read back from HBM, one wave per stream (32 streams per CU), instead
- * of the pipe (0: off) */
+/* CD_FAR_MAX (round 5): values over 4 KiB and up to this size decode with
+ * tokpar64's 4 KiB window (16-bit marks: outputs < 65536) and far sources
+ * read back from HBM, one wave per stream (32 streams per CU), instead of the
+ * pipe (0: off).  16 KiB: Zipf 8 KiB and mixed 16 KiB gain 6-10 %, json
+ * 16 KiB and sentence text 64 KiB lose on their far groups */
 #ifndef CD_FAR_MAX
 #define CD_FAR_MAX 16384u
 #endif
