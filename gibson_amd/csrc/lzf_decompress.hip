@@ -368,6 +368,9 @@ __device__ __forceinline__ void cd_flush(const uint8_t *lds, uint32_t outr_off, 
 #ifndef CD_MARKAHEAD
 #define CD_MARKAHEAD 1
 #endif
+#ifndef CD_ENTGUARD                 /* the doubling loop's guard read off the entries */
+#define CD_ENTGUARD 1
+#endif
 #ifndef CD_FAR2                     /* FAR's one-compare test, its wait on its own path */
 #define CD_FAR2 1
 #endif
@@ -474,7 +477,10 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
          * address (lane × 4) in bits 10-15 */
         const bool pend = !lit && q < CD_LANES;
         int32_t ent = pend ? (int32_t)(q << 10) : (int32_t)(0x80000000u | b);
-        if (cd_ballot(pend)) {
+        /* FAR: the guard read off the entries' sign (== pend, one compare
+         * instead of a select and a compare); measured slower on the pipe and
+         * the plain tokpar64 (instruction placement), so FAR only */
+        if (FAR && CD_ENTGUARD ? cd_ballot(ent >= 0) : cd_ballot(pend)) {
             const int32_t me = (int32_t)(lane << 2);
             do
                 ent = __builtin_amdgcn_ds_bpermute(ent < 0 ? me : ent >> 8, ent);
