@@ -159,7 +159,7 @@ def test_batch_decompress_golden(golden, oracle):
 
 def test_batch_decompress_golden_per_window(golden, oracle):
     # the decoder instance follows the batch's largest out_len (tokpar64 per
-    # window of 256 B .. 4 KiB, the pipe past that): the golden decoder
+    # window of 256 B .. 4 KiB, the FAR route past that up to 16 KiB): the golden decoder
     # corpus (valid, tight, truncated, corrupted, random streams) split into
     # one batch per window size, so every instance meets the error cases
     from tests.gpu_batch import gpu_decompress
@@ -177,6 +177,23 @@ def test_batch_decompress_golden_per_window(golden, oracle):
                for (c, s), (out, e) in zip(cases, res)
                if (len(out) if out else 0) != c["result"] or e != c["errno"] or (out and sha16(out) != c["out_sha"])]
         assert not bad, f"window {w}: {len(bad)} mismatches of {len(cases)}, first: {bad[:5]}"
+
+
+def test_batch_decompress_golden_on_pipe(golden, oracle):
+    # the golden decoder corpus stops at 10 000-byte outputs, so its batches
+    # take tokpar64 and the FAR route; one extra 20 000-byte value lifts the
+    # batch's max_len past CD_FAR_MAX and every case through the pipe
+    from tests.gpu_batch import gpu_decompress
+    from tests.test_oracle import decoder_cases
+    cases = list(decoder_cases(golden, oracle))
+    extra = synth(2, 0x5EED0003, 7, 20000)
+    xs = oracle.compress(extra, len(extra) + 64)
+    res = gpu_decompress([s for _, s in cases] + [xs], [c["out_len"] for c, _ in cases] + [20000])
+    assert res[-1] == (extra, 0)
+    bad = [(c.get("tag"), c["result"], c["errno"], len(out) if out else 0, e)
+           for (c, s), (out, e) in zip(cases, res)
+           if (len(out) if out else 0) != c["result"] or e != c["errno"] or (out and sha16(out) != c["out_sha"])]
+    assert not bad, f"{len(bad)} mismatches of {len(cases)}, first: {bad[:5]}"
 
 
 def test_decoded_size_prepass_golden(golden, oracle):
