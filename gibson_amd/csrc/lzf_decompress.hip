@@ -576,7 +576,9 @@ __device__ __forceinline__ bool cd_refused(const LzfBatch &bt, uint32_t v, uint3
 
 /* CD_TP_SMALL: windows up to 4 KiB (the output stays below 65536, so 16-bit
  * start marks match only in their group: cd_refused holds out_cap to the
- * batch's max_len, and lzf_launch_decompress picks no window below max_len) keep 16-bit marks and compute token
+ * batch's max_len, and lzf_launch_decompress picks no window below max_len;
+ * the FAR route runs the 4 KiB instance past its window only while max_len
+ * <= 65536, checked at its launch) keep 16-bit marks and compute token
  * sizes instead of reading the 256-byte table: 5008 bytes of LDS for a 4 KiB
  * window, 32 streams per CU (the wave limit) instead of 30 */
 #ifndef CD_TP_SMALL
