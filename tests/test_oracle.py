@@ -147,3 +147,34 @@ def test_oracle_config0_fixture(oracle):
     assert len(s) == c["stream_len"] and hashlib.sha256(s).hexdigest() == c["stream_sha256"]
     out, e = oracle.decompress(s, c["decode_out_len"])
     assert out == v and e == c["decode_errno"]
+
+
+def test_far_route_predicate_and_flush_invariant():
+    # the FAR decoder route (gibson_amd/csrc/lzf_decompress.hip, CD_FAR2)
+    # decides "read this byte from HBM" with one add and one unsigned compare
+    # on the owner token's info tInf (a back-reference's distance, 1..8192,
+    # src/lzf_d.c:95; a literal's info has bit 31 set): restated here on every
+    # distance and lane against the window rule it replaces (the source lies
+    # more than the 4 KiB window behind the group's first byte), and the far
+    # source checked to lie in output the 1 KiB flush units already stored
+    import numpy as np
+    window, unit = 4096, 1024
+    omask = window - 1
+    lane = np.arange(64, dtype=np.uint64)[None, :]
+    t_ref = np.arange(1, 8193, dtype=np.uint64)[:, None]
+    t_lit = (np.uint64(1 << 31) + np.arange(0, 4096, 7, dtype=np.uint64))[:, None]
+    for gb in (64 * 64, 64 * 65, 64 * 128, 64 * 200, 64 * 1023):
+        for tinf, lit in ((t_ref, False), (t_lit, True)):
+            m = np.uint64(0xFFFFFFFF)
+            o = np.uint64(gb) + lane
+            so = (o - tinf) & m
+            old = (not lit) & (so < gb) & (((np.uint64(gb) - so) & m) > window)
+            new = np.broadcast_to(((tinf - lane - np.uint64(omask + 2)) & m) < np.uint64(8191 - omask), old.shape)
+            # a reference before the output start fails in the round's decode
+            # (EINVAL, src/lzf_d.c:127-130) and never reaches the output step
+            valid = np.broadcast_to(lit | (tinf <= o), old.shape)
+            assert np.array_equal(old[valid], new[valid]), gb
+            if not lit:
+                flushed = (gb // unit) * unit          # every group before gb is done
+                far_so = so[new & valid]
+                assert (far_so + 128 <= flushed).all()
