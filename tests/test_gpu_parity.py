@@ -743,15 +743,16 @@ def test_decode_self_overlapping_references(oracle):
     assert gpu_decompress(streams, [len(v) for v in vals]) == [(v, 0) for v in vals]
 
 
-@pytest.mark.parametrize("nmax", [8192, 16384, 16385])
-def test_decode_far_sources(oracle, nmax):
+@pytest.mark.parametrize("nmax,align", [(8192, 16), (16384, 16), (16385, 16), (16384, 3)])
+def test_decode_far_sources(oracle, nmax, align):
     # batches whose largest value is 4-16 KiB decode on the 4 KiB tokpar
     # window with sources more than 4 KiB behind the output group read back
     # from dst in HBM (CD_FAR_MAX); 16385 takes the 8 KiB pipe instead.  A
     # random block repeated at distances 4095..8192 (the LZF maximum, src/
     # lzf_d.c:121) puts copies on both sides of the window edge, self-
     # overlapping runs straddle it, and values at the batch maximum share the
-    # launch with tiny ones
+    # launch with tiny ones; align 3 packs streams and output regions at
+    # multiples of 3 bytes (far loads and 16-byte flushes off alignment)
     from tests.gpu_batch import gpu_decompress
     rnd = random.Random(nmax)
     vals = []
@@ -771,7 +772,7 @@ def test_decode_far_sources(oracle, nmax):
     streams = [oracle.compress(v, len(v) + len(v) // 16 + 64) if v else b"" for v in vals]
     assert all(s or not v for s, v in zip(streams, vals))
     keep = [i for i, v in enumerate(vals) if v]
-    got = gpu_decompress([streams[i] for i in keep], [len(vals[i]) for i in keep])
+    got = gpu_decompress([streams[i] for i in keep], [len(vals[i]) for i in keep], align=align)
     assert got == [(vals[i], 0) for i in keep]
     # the same streams truncated: the errno the reference returns on the
     # FAR route's batches (src/lzf_d.c:79-82, 110-114, 127-130)
@@ -780,7 +781,7 @@ def test_decode_far_sources(oracle, nmax):
         s = streams[i]
         bad_s.append(s[:len(s) * 2 // 3])
         bad_l.append(len(vals[i]))
-    res = gpu_decompress(bad_s, bad_l)
+    res = gpu_decompress(bad_s, bad_l, align=align)
     for s, n, (out, e) in zip(bad_s, bad_l, res):
         ref = oracle.decompress(s, n)
         assert (out, e) == ref
