@@ -371,6 +371,9 @@ __device__ __forceinline__ void cd_flush(const uint8_t *lds, uint32_t outr_off, 
 #ifndef CD_ENTGUARD                 /* the doubling loop's guard read off the entries */
 #define CD_ENTGUARD 1
 #endif
+#ifndef CD_FARB
+#define CD_FARB 1
+#endif
 #ifndef CD_FAR2                     /* FAR's one-compare test, its wait on its own path */
 #define CD_FAR2 1
 #endif
@@ -399,7 +402,10 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
 #endif
     /* lanes without a token mark slot 64 (never read): their start lies 2^31 away */
     const uint32_t Otm = tok ? Ot : Ot + 0x80000000u;
-    const uint32_t farb = 0u - (lane + omask + 2u);   /* FAR: tInf - lane - (window + 1) */
+    uint32_t farb = 0u - (lane + omask + 2u);         /* FAR: tInf - lane - (window + 1) */
+#if CD_FARB
+    if (FAR) asm volatile("" : "+v"(farb));          /* kept whole: one add per group, not a subtract and an add */
+#endif
     /* a start mark holds the token's own start, so it matches only in its
      * group (no per-group tag; position 0, the unwritten marks' 0, always
      * starts a token) */
