@@ -75,10 +75,18 @@ def parse():
     ap.add_argument("--total", type=int, default=0,
                     help="strong scaling: values over all ranks (rank r takes values r, r+N, ...)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--config4", action="store_true",
+                    help="also measure BASELINE configs[4] (4M x 16 KiB over the ranks) into a config4 "
+                         "block; on by default when N > 1 on the default workload")
+    ap.add_argument("--no-config4", action="store_true", help="skip the configs[4] block at N > 1")
+    ap.add_argument("--config4-total", type=int, default=4 << 20,
+                    help="values of the configs[4] block over all ranks (default 4194304, BASELINE configs[4])")
     ap.add_argument("--cpu-count", type=int, default=0, help="CPU baseline sample values")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (default: the cores this process may run on)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    a.workload_given = bool(a.workload)
+    return a
 
 
 def launch_ranks(a):
@@ -244,7 +252,75 @@ def main():
     if a.mode == "decompress":
         return main_decompress(a, world, rank, dev, cfg_idx, kind, seed, n, count)
 
-    # ---- data in HBM: value i of this rank is global value rank + k*world ----
+    rt = run_roundtrip(a, world, rank, dev, kind, seed, n, count)
+    line = roundtrip_line(a, world, rank, rt, cfg_idx, kind, seed, n, count)
+    # N > 1 on the default workload: the driver's 1 -> 8 curve stays on
+    # configs[2] (weak scaling, the `value` every N reports), and the line also
+    # carries configs[4] -- 4 M x 16 KiB split over the ranks, the config the
+    # north star's >= 0.9x per-GPU efficiency target is stated on
+    #  -- measured in the same job, with its per-GPU
+    # efficiency against the committed N = 1 figure
+    if wants_config4(a, world):
+        del rt
+        gibson_amd.release()
+        torch.cuda.empty_cache()
+        c_idx, c_kind, c_seed, c_n, _ = WORKLOADS["mixed16k"]
+        c_total = a.config4_total
+        c_count = (c_total - rank + world - 1) // world
+        r4 = run_roundtrip(a, world, rank, dev, c_kind, c_seed, c_n, c_count)
+        if rank == 0:
+            line["config4"] = config4_block(world, r4, c_total, c_n)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+CONFIG4_TOTAL = 4 << 20          # BASELINE configs[4]: 4 M x 16 KiB values over all ranks
+CONFIG4_N1 = os.path.join(ROOT, "profiles", "r06", "config4_n1.json")
+
+
+def wants_config4(a, world):
+    """whether the line carries the configs[4] block: asked for (--config4),
+    or N > 1 on the default round-trip workload (the driver's scaling runs),
+    unless --no-config4"""
+    if a.no_config4 or a.mode != "roundtrip":
+        return False
+    return a.config4 or (world > 1 and not (a.workload_given or a.total or a.count))
+
+
+def config4_block(world, r4, total, n):
+    """configs[4]'s strong split measured beside the headline: aggregate
+    GB/s over all ranks, and per-GPU efficiency = value / (N x the N = 1
+    figure committed in profiles/r06/config4_n1.json, `bench.py --workload
+    mixed16k --total 4194304` on one MI355X)"""
+    sec = r4["wall"] / r4["steps"]
+    value = r4["in_bytes_all"] / sec / 1e9
+    blk = {"config": "BASELINE configs[4]: 4M x 16 KiB mixed-entropy values sharded round-robin over "
+                     f"{world} rank(s) (strong scaling; the north star's >= 0.9x per-GPU efficiency target)",
+           "baseline_config": 4, "total_values": total, "values_per_gpu_max": -(-total // world),
+           "value": round(value, 3), "unit": "GB/s", "ms_per_step": round(sec * 1e3, 3),
+           "roundtrip_ok": r4["bad_ranks"] == 0, "chunks_per_rank": r4["nch"],
+           "per_kernel_ms_rank0": {"lzf_compress": round(r4["t_comp"] * 1e3, 3),
+                                   "lzf_decompress": round(r4["t_dec"] * 1e3, 3)}}
+    try:
+        ref = json.load(open(CONFIG4_N1))
+        v1 = float(ref["value"])
+        blk["n1_value"] = v1
+        blk["n1_source"] = os.path.relpath(CONFIG4_N1, ROOT)
+        # only against the figure of the same configuration
+        blk["per_gpu_efficiency"] = round(value / (world * v1), 4) if total == ref.get("total_values") else None
+    except (OSError, KeyError, ValueError):
+        blk["n1_value"] = None
+        blk["per_gpu_efficiency"] = None
+    return blk
+
+
+def run_roundtrip(a, world, rank, dev, kind, seed, n, count):
+    """One workload's timed round trips on this rank: value k of this rank is
+    global value rank + k*world, generated into HBM; a step compresses every
+    value (out_len n-4) and decodes every success.  Returns this rank's
+    timings and counts and the job-wide reductions."""
     # A batch past CHUNK_BYTES (BASELINE configs[4] at N = 1: 4 M x 16 KiB =
     # 64 GiB) keeps every input and stream resident but runs the codec in
     # chunks of <= 16 GiB (SURVEY.md §8(d) timing rules): the kernels' scratch
@@ -328,76 +404,92 @@ def main():
     good = verify(c0, count - c0) and good
 
     (k_lo, w_lo), (k_hi, w_hi) = spread_stats([t_comp + t_dec, wall], device=RED_DEV)
-    (wall, t_comp, t_dec), (in_bytes_all, n_ok_all, c_bytes_all, bad_ranks) = reduce_stats(
+    (wall, t_comp_max, t_dec_max), (in_bytes_all, n_ok_all, c_bytes_all, bad_ranks) = reduce_stats(
         [wall, t_comp, t_dec], [count * n, n_ok, c_bytes, 0 if good else 1], device=RED_DEV)
+    return {"wall": wall, "steps": a.steps, "t_comp": t_comp, "t_dec": t_dec, "n_ok": n_ok, "c_bytes": c_bytes,
+            "in_bytes_all": in_bytes_all, "n_ok_all": n_ok_all, "c_bytes_all": c_bytes_all,
+            "bad_ranks": bad_ranks, "nch": nch, "chunk": chunk,
+            "spread": (k_lo, k_hi, w_lo, w_hi)}
 
-    if rank == 0:
-        sec_per_step = wall / a.steps
-        value = in_bytes_all / sec_per_step / 1e9
-        # algorithmic bytes per launch, this rank
-        comp_bytes = count * n + c_bytes + 4 * count          # read N, write C + 4
-        dec_bytes = c_bytes + n_ok * n                          # read C, write N
-        kern = {
-            "lzf_compress": (comp_bytes, t_comp),
-            "lzf_decompress": (dec_bytes, t_dec),
-        }
-        dom = max(kern, key=lambda k: kern[k][1])
-        ach = kern[dom][0] / kern[dom][1] / 1e9
-        line = {
-            "metric": "LZF GB/s (device-resident) over batched value blocks, compress+decompress",
-            "value": round(value, 3),
+
+def roundtrip_line(a, world, rank, rt, cfg_idx, kind, seed, n, count):
+    """rank 0's JSON line for a round-trip run (None on other ranks)"""
+    if rank != 0:
+        return None
+    wall, t_comp, t_dec = rt["wall"], rt["t_comp"], rt["t_dec"]
+    n_ok, c_bytes = rt["n_ok"], rt["c_bytes"]
+    sec_per_step = wall / a.steps
+    value = rt["in_bytes_all"] / sec_per_step / 1e9
+    # algorithmic bytes per launch (SURVEY.md §8(d)), this rank
+    comp_bytes = count * n + c_bytes + 4 * count          # read N, write C + 4
+    dec_bytes = c_bytes + n_ok * n                          # read C, write N
+    kern = {
+        "lzf_compress": (comp_bytes, t_comp),
+        "lzf_decompress": (dec_bytes, t_dec),
+    }
+    dom = max(kern, key=lambda k: kern[k][1])
+    ach = kern[dom][0] / kern[dom][1] / 1e9
+    # the north star's compress + decompress at once: 2N + 2C + 4 per value
+    # over all ranks (compress reads N, writes C + 4; decode reads C, writes N)
+    # over the step's wall time, per GPU, against the per-GPU peak
+    rt_bytes_all = 2 * rt["in_bytes_all"] + 2 * rt["c_bytes_all"] + 4 * count * world
+    roundtrip_frac = rt_bytes_all / sec_per_step / 1e9 / (HBM_PEAK_GBPS * world)
+    k_lo, k_hi, w_lo, w_hi = rt["spread"]
+    line = {
+        "metric": "LZF GB/s (device-resident) over batched value blocks, compress+decompress",
+        "value": round(value, 3),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(sec_per_step * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong" if a.total else "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {
+            "workload": DESCR[a.workload] if not a.total else
+                        f"{a.total} x {n // 1024} KiB values over all ranks ({DESCR[a.workload]})",
+            "baseline_config": cfg_idx,
+            "values_per_gpu": count,
+            "value_bytes": n,
+            "out_len_policy": "n-4 (src/query.c:385)",
+            "sharding": "round-robin value i -> rank i mod N, no collective",
+            "compressed_fraction": round(rt["n_ok_all"] / (count * world), 4),
+            "ratio": round(rt["c_bytes_all"] / max(1.0, rt["n_ok_all"] * n), 4),
+            "kernels": gibson_amd.kernel_info(),
+            "roundtrip_ok": rt["bad_ranks"] == 0,
+            "chunks": rt["nch"],
+            "chunk_values": rt["chunk"],
+        },
+        "rank_spread": _spread(world, a.steps, k_lo, k_hi, w_lo, w_hi),
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom,
+            "achieved": round(ach, 2),
+            "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(sec_per_step * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "strong" if a.total else "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic",
-            "config": {
-                "workload": DESCR[a.workload] if not a.total else
-                            f"{a.total} x {n // 1024} KiB values over all ranks ({DESCR[a.workload]})",
-                "baseline_config": cfg_idx,
-                "values_per_gpu": count,
-                "value_bytes": n,
-                "out_len_policy": "n-4 (src/query.c:385)",
-                "sharding": "round-robin value i -> rank i mod N, no collective",
-                "compressed_fraction": round(n_ok_all / (count * world), 4),
-                "ratio": round(c_bytes_all / max(1.0, n_ok_all * n), 4),
-                "kernels": gibson_amd.kernel_info(),
-                "roundtrip_ok": bad_ranks == 0,
-                "chunks": nch,
-                "chunk_values": chunk,
-            },
-            "rank_spread": _spread(world, a.steps, k_lo, k_hi, w_lo, w_hi),
-            "roofline": {
-                "bound": "hbm",
-                "kernel": dom,
-                "achieved": round(ach, 2),
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBPS, 5),
-                "traffic": _traffic(a.workload, dom, count)[0],
-                "traffic_source": _traffic(a.workload, dom, count)[1],
-                "algorithmic_bytes": kern[dom][0],
-                "per_kernel_ms": {k: round(v[1] * 1e3, 3) for k, v in kern.items()},
-                "per_kernel_GBps": {k: round(v[0] / v[1] / 1e9, 2) for k, v in kern.items()},
-                # the round trip's read-only fraction, sum(N + C) / t / peak
-                "read_only_frac": round((count * n + c_bytes) / (t_comp + t_dec) / 1e9 / HBM_PEAK_GBPS, 5),
-            },
-        }
-        if world == 1 and not a.no_cpu:
-            cores, note = cpu_cores()
-            threads = a.cpu_threads or cores
-            cnt = a.cpu_count or min(count, max(4 * threads, (4 << 30) // n))
-            line["cpu_baseline"] = cpu_baseline(kind, seed, n, cnt, threads)
-            if line["cpu_baseline"] and "error" not in line["cpu_baseline"]:
-                line["cpu_baseline"]["cores_note"] = note
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+            "frac": round(ach / HBM_PEAK_GBPS, 5),
+            "roundtrip_frac": round(roundtrip_frac, 5),
+            "roundtrip_bytes_per_value": "2N + 2C + 4 (compress reads N, writes C + 4; decode reads C, writes N)",
+            "traffic": _traffic(a.workload, dom, count)[0],
+            "traffic_source": _traffic(a.workload, dom, count)[1],
+            "algorithmic_bytes": kern[dom][0],
+            "per_kernel_ms": {k: round(v[1] * 1e3, 3) for k, v in kern.items()},
+            "per_kernel_GBps": {k: round(v[0] / v[1] / 1e9, 2) for k, v in kern.items()},
+            # SURVEY.md §8(d): the round trip's read-only fraction, sum(N + C) / t / peak
+            "read_only_frac": round((count * n + c_bytes) / (t_comp + t_dec) / 1e9 / HBM_PEAK_GBPS, 5),
+        },
+    }
+    if world == 1 and not a.no_cpu:
+        cores, note = cpu_cores()
+        threads = a.cpu_threads or cores
+        cnt = a.cpu_count or min(count, max(4 * threads, (4 << 30) // n))
+        line["cpu_baseline"] = cpu_baseline(kind, seed, n, cnt, threads)
+        if line["cpu_baseline"] and "error" not in line["cpu_baseline"]:
+            line["cpu_baseline"]["cores_note"] = note
+    return line
 
 
 def main_decompress(a, world, rank, dev, cfg_idx, kind, seed, n, count):

@@ -34,6 +34,8 @@ from .lzf import (  # noqa: F401
     device_plan,
     host_last_spread,
     host_split,
+    host_split_block,
+    host_split_policy,
     parse_device_list,
     kv_frame,
 )

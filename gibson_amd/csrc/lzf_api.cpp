@@ -148,6 +148,11 @@ struct Scratch {
     hipEvent_t ev = nullptr;
     hipStream_t last = nullptr;
     bool used = false;
+    /* this scratch's share of the cap: 1 for the device's, NSLOT for each
+     * chunk slot of the registered host pipeline, whose launches run side by
+     * side and keep their buffers between calls -- together they stay within
+     * one cap instead of taking half of what each one finds free */
+    unsigned share = 1;
 #ifdef LZF_DIAG
     hipStream_t aux = nullptr;      /* kernel-2 stream of the chunk pipeline */
     hipEvent_t pev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -160,17 +165,22 @@ Scratch g_scratch[64];
  * free when the scratch grows (at least 1 GiB): a whole BASELINE batch
  * (256 K x 64 KiB: 67 GiB of records) then runs as one chunk, and a caller
  * that holds most of the device still gets chunked, not refused. */
-size_t scratch_limit(size_t held)
+size_t scratch_limit(size_t held, unsigned share = 1)
 {
+    if (share < 1) share = 1;
     const char *e = getenv("LZF_GPU_SCRATCH_MB");
     if (e) {
         unsigned long long mb = strtoull(e, nullptr, 10);
         if (mb < 1) mb = 1;
-        return (size_t)mb << 20;
+        return ((size_t)mb << 20) / share;
     }
     size_t fr = 0, tot = 0;
-    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return (size_t)40 << 30;
-    size_t lim = (fr + held) / 2;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return ((size_t)40 << 30) / share;
+    /* held: this scratch's own buffer, which a regrow gives back first; the
+     * slot scratches' shares are of the device's total, so buffers the other
+     * slots already hold do not shrink the next one's share */
+    size_t lim = share == 1 ? (fr + held) / 2 : tot / (2 * (size_t)share);
+    if (share > 1 && lim > fr + held) lim = fr + held;
     return lim > ((size_t)1 << 30) ? lim : ((size_t)1 << 30);
 }
 
@@ -207,7 +217,7 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s, ScratchUser who, Scra
     const size_t per = table ? lzf_table_scratch_per_value(b.max_len) : lzf_lane_scratch_per_value(b.max_len);
 #endif
     size_t want = per * (size_t)b.count + 512;
-    const size_t lim = scratch_limit(S.cap);
+    const size_t lim = scratch_limit(S.cap, S.share);
     if (want > lim) want = lim;
     if (want < 2 * per + 1024) want = 2 * per + 1024;     /* two pipeline halves */
     /* an explicit cap binds even when an earlier batch grew the scratch past
@@ -332,8 +342,16 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s, Scratch *own = null
             if (!lane && lzf_lane_compress_supported(b.max_len)) {
                 int dev = 0;
                 if (hipGetDevice(&dev) == hipSuccess) {
-                    const Scratch &S = own ? *own : g_scratch[dev & 63];
-                    const size_t lim = scratch_limit(S.cap);
+                    Scratch &S = own ? *own : g_scratch[dev & 63];
+                    size_t held;
+                    unsigned share;
+                    {
+                        /* another thread's lane_compress may be regrowing it */
+                        std::lock_guard<std::mutex> lk(S.mu);
+                        held = S.cap;
+                        share = S.share;
+                    }
+                    const size_t lim = scratch_limit(held, share);
                     const uint64_t need_t = (uint64_t)b.count * lzf_table_scratch_per_value(b.max_len);
                     const uint64_t need_l = (uint64_t)b.count * lzf_lane_scratch_per_value(b.max_len);
                     lane = (need_t + lim - 1) / lim > (need_l + lim - 1) / lim;
@@ -390,7 +408,12 @@ hipError_t lzf_route_compress_bulk(const LzfBatch &b, hipStream_t s, void *scrat
 {
     return launch_compress(b, s, (Scratch *)scratch, true);
 }
-void *lzf_scratch_create(void) { return new Scratch(); }
+void *lzf_scratch_create(unsigned share)
+{
+    Scratch *S = new Scratch();
+    S->share = share ? share : 1u;
+    return S;
+}
 void lzf_scratch_destroy(void *scratch)
 {
     Scratch *S = (Scratch *)scratch;

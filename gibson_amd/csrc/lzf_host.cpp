@@ -324,6 +324,37 @@ Ctx &caller_ctx()
 
 /* ---- registered host ranges (lzf_host_register) --------------------------- */
 
+/* every distinct device of the plan maps [ptr, ptr + len): a device address
+ * for its first and last byte, on that device (LZF_GPU_ENODEV otherwise; the
+ * registration is then undone).  LZF_GPU_FORCE_MAP_FAIL=<device> makes that
+ * device's check fail (the tests of the refusal). */
+int register_check_devices(const std::vector<int> &devs, const void *ptr, uint64_t len)
+{
+    const char *ff = getenv("LZF_GPU_FORCE_MAP_FAIL");
+    const int force = ff && *ff ? atoi(ff) : -1;
+    std::vector<int> seen;
+    for (int d : devs) {
+        bool dup = false;
+        for (int x : seen) dup = dup || x == d;
+        if (dup) continue;
+        seen.push_back(d);
+        if (hipSetDevice(d) != hipSuccess) {
+            (void)hipGetLastError();
+            return LZF_GPU_ENODEV;
+        }
+        void *p0 = nullptr, *p1 = nullptr;
+        const bool ok = hipHostGetDevicePointer(&p0, (void *)ptr, 0) == hipSuccess &&
+                        hipHostGetDevicePointer(&p1, (void *)((const uint8_t *)ptr + len - 1), 0) == hipSuccess &&
+                        p0 && (uintptr_t)p1 - (uintptr_t)p0 == len - 1 && d != force;
+        if (!ok) {
+            (void)hipGetLastError();
+            fprintf(stderr, "liblzf_hip: registered range not mapped on device %d\n", d);
+            return LZF_GPU_ENODEV;
+        }
+    }
+    return LZF_GPU_OK;
+}
+
 std::mutex g_reg_mu;
 std::map<uintptr_t, uintptr_t> g_reg;      /* start -> end of each registered range */
 
@@ -399,7 +430,7 @@ void make_slot_streams(Ctx &c)
     for (auto &sl : c.slot) {
         if (!sl.stream) check(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking), "hipStreamCreate");
         if (!sl.done) check(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming), "hipEventCreate");
-        if (!sl.scratch) sl.scratch = lzf_scratch_create();
+        if (!sl.scratch) sl.scratch = lzf_scratch_create(NSLOT);   /* the slots share one cap */
         if (!sl.in_done) check(hipEventCreateWithFlags(&sl.in_done, hipEventDisableTiming), "hipEventCreate");
         if (!sl.out_done) check(hipEventCreateWithFlags(&sl.out_done, hipEventDisableTiming), "hipEventCreate");
         sl.busy = false;
@@ -614,8 +645,8 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
     }
     uint32_t nchunks = 1;
     bool bulk = false;
+    uint64_t chunk_bytes = 4096ull << 20;                  /* compress: the largest chunk's input */
     if (a.compress) {
-        uint64_t chunk_bytes = 2048ull << 20;
         if (const char *e = getenv("LZF_GPU_HOST_CHUNK_MB")) chunk_bytes = (uint64_t)strtoull(e, nullptr, 10) << 20;
         if (chunk_bytes < (1u << 20)) chunk_bytes = 1u << 20;
         if (total >= (192ull << 20) && v.count >= NSLOT * 1024u) {
@@ -638,7 +669,29 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
      * the last chunk's cand and scatter are short, were slower -- text64k
      * 202 -> 211 ms, json4k 62 -> 66 -- its cand squeezes between running
      * parses either way, and the parse's floor does not shrink with it) */
-    std::vector<uint32_t> bound;
+    std::vector<uint32_t> bound{0u};
+    /* [lo, hi) as `parts` chunks of about equal bytes (value-aligned, none
+     * empty), boundaries appended to `bound` */
+    auto split_bytes = [&](uint32_t lo, uint32_t hi, uint32_t parts) {
+        auto bytes_of = [&](uint32_t k) -> uint64_t { return a.compress ? a.in_len[v.at(k)] : a.out_cap[v.at(k)]; };
+        uint64_t tot = 0;
+        for (uint32_t k = lo; k < hi; k++) tot += bytes_of(k);
+        if (parts > hi - lo) parts = hi - lo;
+        uint64_t acc = 0;
+        uint32_t k = lo;
+        for (uint32_t p = 1; p < parts; p++) {
+            const uint64_t target = tot * p / parts;
+            while (k < hi && acc + bytes_of(k) <= target) acc += bytes_of(k++);
+            if (k == bound.back() && k < hi) acc += bytes_of(k++);     /* never an empty chunk */
+            if (k < hi) bound.push_back(k);
+        }
+        if (bound.back() != hi) bound.push_back(hi);
+    };
+    auto bytes_in = [&](uint32_t lo, uint32_t hi) {
+        uint64_t t = 0;
+        for (uint32_t k = lo; k < hi; k++) t += a.compress ? a.in_len[v.at(k)] : a.out_cap[v.at(k)];
+        return t;
+    };
     /* Tail mode (compress, values over 16 KiB): the first part of the batch
      * goes through the routed generations as one chunk, whose parse -- a
      * per-value chain of ~70 ms for 64 KiB values whatever the count --
@@ -648,7 +701,10 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
      * its own input, the last one after all of it.  The
      * routed part's share: LZF_GPU_HOST_TAIL (percent of the values, default
      * 70; 0 turns the mode off); window64 chunks: LZF_GPU_HOST_TAIL_CHUNKS
-     * (1-4, default 1).  Registered text64k, 64 K values, compress GB/s
+     * (1-4, default 1).  Both parts keep the chunk cap (LZF_GPU_HOST_CHUNK_MB,
+     * default 4096): a routed share or window64 part past it is split into
+     * chunks of at most that many input bytes, and chunks past the slots
+     * reuse them in turn.  Registered text64k, 64 K values, compress GB/s
      * (profiles/r05/host_text64k_reg_tail*, tail_chunks/): four window
      * chunks by share: off 20.8, 30 % 21.6, 40 % 22.6, 50 % 23.9, 60 % 24.3,
      * 70 % 24.3, 80 % 23.0, 90 % 21.7; at 70 %, 1 / 2 / 3 / 4 chunks: 24.9 /
@@ -664,12 +720,12 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         if (const char *e = getenv("LZF_GPU_HOST_TAIL_CHUNKS")) TAIL_CHUNKS = (uint32_t)strtoul(e, nullptr, 10);
         if (TAIL_CHUNKS < 1u) TAIL_CHUNKS = 1u;
         if (TAIL_CHUNKS > TAIL_MAX) TAIL_CHUNKS = TAIL_MAX;
-        bound.push_back(0u);
-        bound.push_back(tail_from);
-        for (uint32_t k = 1; k <= TAIL_CHUNKS; k++)
-            bound.push_back(tail_from + (uint32_t)((uint64_t)(v.count - tail_from) * k / TAIL_CHUNKS));
+        const uint64_t rb = bytes_in(0u, tail_from), tb = bytes_in(tail_from, v.count);
+        split_bytes(0u, tail_from, (uint32_t)((rb + chunk_bytes - 1) / chunk_bytes));
+        const uint32_t tcap = (uint32_t)((tb + chunk_bytes - 1) / chunk_bytes);
+        split_bytes(tail_from, v.count, TAIL_CHUNKS > tcap ? TAIL_CHUNKS : tcap);
     } else {
-        for (uint32_t k = 0; k <= nchunks; k++) bound.push_back((uint32_t)((uint64_t)v.count * k / nchunks));
+        split_bytes(0u, v.count, nchunks);
     }
     const uint32_t min_len = a.compress ? 0u : 1u;
 
@@ -693,12 +749,15 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
     uint32_t round = 0;
     for (; round + 1 < bound.size(); round++) {
         const uint32_t k0 = bound[round], n = bound[round + 1] - k0;
-        /* tail mode: slot 0 for the routed chunk (it finishes last), one slot
-         * each for the window64 chunks, so every chunk's input crosses the bus
-         * as soon as the one before it is in (with two slots for four chunks,
-         * the third waited for the first's kernel: profiles/r05/tail_chunks/) */
-        const uint32_t si = tail_from == v.count ? round % NSLOT : round;
-        const uint32_t prev_si = round == 0u ? 0u : tail_from == v.count ? (round - 1u) % NSLOT : round - 1u;
+        /* tail mode: every chunk its own slot while they last (the routed
+         * chunk in slot 0 finishes last), so every chunk's input crosses the
+         * bus as soon as the one before it is in (with two slots for four
+         * chunks, the third waited for the first's kernel:
+         * profiles/r05/tail_chunks/); past NSLOT_ALL chunks (a chunk cap far
+         * below the batch) slots are reused in turn after draining */
+        const uint32_t ns = tail_from == v.count ? NSLOT : NSLOT_ALL;
+        const uint32_t si = round % ns;
+        const uint32_t prev_si = round == 0u ? 0u : (round - 1u) % ns;
         Slot &sl = c.slot[si];
         drain(sl);
         uint8_t *h_meta = (uint8_t *)sl.h_meta.get((size_t)n * mrec);
@@ -815,6 +874,10 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         if (round && CHAIN_OUT && tail_from == v.count)
             check(hipStreamWaitEvent(sl.stream, c.slot[prev_si].out_done, 0), "hipStreamWaitEvent");
         if (!a.compress && oruns.size() <= few) {
+            /* a run carries whole slots: zero each slot past its decoded
+             * length first, so no stale device bytes (an earlier chunk's or
+             * batch's values) reach the caller's memory */
+            check(lzf_launch_clear_tail(d_out, d_dout, d_out_len, d_cap, n, sl.stream), "clear launch");
             for (const Run &r : oruns)
                 if (r.len)
                     check(hipMemcpyAsync(a.out + r.host, d_out + r.dev, r.len, hipMemcpyDeviceToHost, sl.stream),
@@ -994,14 +1057,22 @@ struct Worker {
 };
 
 /* one worker per plan entry, made on first use and kept for the process's
- * life (its thread waits on its queue; process exit ends it) */
+ * life (its thread waits on its queue; process exit ends it).  Returns only
+ * with every entry's worker made: when making one throws (a thread or memory
+ * that could not be had), the vector keeps the workers made so far, the
+ * exception reaches the caller (who returns LZF_GPU_ENOMEM), and the next
+ * call goes on from there -- no caller ever sees a partial plan. */
 std::vector<Worker *> &workers()
 {
     static std::mutex mu;
     static std::vector<Worker *> w;
     std::lock_guard<std::mutex> lk(mu);
-    if (w.empty())
-        for (int d : plan().dev) w.push_back(new Worker(d));
+    const std::vector<int> &dev = plan().dev;
+    while (w.size() < dev.size()) {
+        std::unique_ptr<Worker> x(new Worker(dev[w.size()]));
+        w.push_back(x.get());
+        x.release();
+    }
     return w;
 }
 
@@ -1039,6 +1110,7 @@ int dispatch(uint32_t count, const std::function<int(Ctx &, const View &)> &job)
     const Plan &P = plan();
     if (P.rc != LZF_GPU_OK) return P.rc;
     const uint32_t G = (uint32_t)P.dev.size();
+    const bool block = lzf_host_split_policy() == 1;
     g_spread.assign(G, Spread{});
     if (G <= 1 || count == 1) {
         const auto t0 = std::chrono::steady_clock::now();
@@ -1061,11 +1133,13 @@ int dispatch(uint32_t count, const std::function<int(Ctx &, const View &)> &job)
         return LZF_GPU_ENOMEM;                     /* a worker thread could not be made */
     }
     std::vector<Worker *> &w = *wp;
+    if (w.size() != G) return LZF_GPU_ENOMEM;
     Join j;
     j.left = G;
     for (uint32_t d = 0; d < G; d++) {
         View v;
-        v.count = lzf_host_split(count, G, d, &v.first, &v.stride);
+        v.count = block ? lzf_host_split_block(count, G, d, &v.first) : lzf_host_split(count, G, d, &v.first, &v.stride);
+        if (block) v.stride = 1u;
         g_spread[d].values = v.count;
         if (!v.count || !w[d]->ctx->ok) {
             j.done(v.count ? LZF_GPU_ENODEV : LZF_GPU_OK);
@@ -1191,8 +1265,23 @@ int lzf_host_register(const void *ptr, uint64_t len)
     int prev = -1;
     (void)hipGetDevice(&prev);
     hipError_t e = hipSetDevice(P.dev[0]);
-    /* portable: every device of the plan maps it */
+    /* portable: registered once, pinned for every device */
     if (e == hipSuccess) e = hipHostRegister((void *)ptr, len, hipHostRegisterMapped | hipHostRegisterPortable);
+    /* and mapped on each device of the plan: a batch's worker asks for the
+     * arena's device address on its own device (host_batch), so the range is
+     * refused here, whole, unless every plan device gives one -- for the
+     * first and the last byte */
+    if (e == hipSuccess) {
+        const int rc = register_check_devices(P.dev, ptr, len);
+        if (rc != LZF_GPU_OK) {
+            (void)hipSetDevice(P.dev[0]);
+            (void)hipHostUnregister((void *)ptr);
+            if (prev >= 0) (void)hipSetDevice(prev);
+            std::lock_guard<std::mutex> lk(g_reg_mu);
+            g_reg.erase(lo);
+            return rc;
+        }
+    }
     if (prev >= 0 && prev != P.dev[0]) (void)hipSetDevice(prev);
     std::lock_guard<std::mutex> lk(g_reg_mu);
     if (e != hipSuccess) {
@@ -1247,13 +1336,36 @@ uint32_t lzf_host_split(uint32_t count, uint32_t groups, uint32_t g, uint32_t *f
     return (count - g + groups - 1u) / groups;
 }
 
+uint32_t lzf_host_split_block(uint32_t count, uint32_t groups, uint32_t g, uint32_t *first)
+{
+    if (!groups || g >= groups) {
+        if (first) *first = 0;
+        return 0;
+    }
+    const uint32_t lo = (uint32_t)((uint64_t)count * g / groups), hi = (uint32_t)((uint64_t)count * (g + 1) / groups);
+    if (first) *first = lo;
+    return hi - lo;
+}
+
+int lzf_host_split_policy(void)
+{
+    const char *e = getenv("LZF_GPU_SPLIT");
+    return e && !strcmp(e, "block") ? 1 : 0;
+}
+
 int lzf_gpu_device_plan(int *device, int *numa_node, int *bound, int max)
 {
     const Plan &P = plan();
     if (P.rc != LZF_GPU_OK) return P.rc;
     const int G = (int)P.dev.size();
     if (G > 1) {
-        std::vector<Worker *> &w = workers();
+        std::vector<Worker *> *wp = nullptr;
+        try {
+            wp = &workers();
+        } catch (...) {
+            return LZF_GPU_ENOMEM;
+        }
+        std::vector<Worker *> &w = *wp;
         for (int k = 0; k < G && k < max; k++) {
             if (device) device[k] = w[k]->dev;
             if (numa_node) numa_node[k] = w[k]->numa;
@@ -1286,7 +1398,13 @@ void lzf_gpu_release(void)
     } catch (const LzfFail &) {
     }
     if (plan().rc == LZF_GPU_OK && plan().dev.size() > 1) {
-        std::vector<Worker *> &w = workers();
+        std::vector<Worker *> *wp = nullptr;
+        try {
+            wp = &workers();
+        } catch (...) {
+            return;                                    /* no complete plan: nothing of it ran */
+        }
+        std::vector<Worker *> &w = *wp;
         Join j;
         j.left = (uint32_t)w.size();
         for (Worker *x : w)

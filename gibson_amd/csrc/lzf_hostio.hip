@@ -67,3 +67,32 @@ hipError_t lzf_launch_move(const uint8_t *src, const uint64_t *src_off, uint8_t 
                        count);
     return hipGetLastError();
 }
+
+/* Registered decode: the slots of values whose outputs abut go back to the
+ * caller as one DMA run of their whole capacity.  The bytes of a slot past
+ * its decoded length (a short or failed decode) would then carry whatever an
+ * earlier chunk or batch left in the device arena -- other requests' values.
+ * They are zeroed first, so a DMA run writes only this value's bytes and
+ * zeros.  One workgroup per value (grid-stride); most slots are full
+ * (out_len == cap) and return at once. */
+__global__ __launch_bounds__(256) void lzf_clear_tail_kernel(uint8_t *__restrict__ dst,
+                                                             const uint64_t *__restrict__ dst_off,
+                                                             const uint32_t *__restrict__ len,
+                                                             const uint32_t *__restrict__ cap, uint32_t count)
+{
+    for (uint32_t k = blockIdx.x; k < count; k += gridDim.x) {
+        const uint32_t lo = len[k], hi = cap[k];
+        if (lo >= hi) continue;
+        uint8_t *d = dst + dst_off[k];
+        for (uint32_t j = lo + threadIdx.x; j < hi; j += blockDim.x) d[j] = 0u;
+    }
+}
+
+hipError_t lzf_launch_clear_tail(uint8_t *dst, const uint64_t *dst_off, const uint32_t *len, const uint32_t *cap,
+                                 uint32_t count, hipStream_t s)
+{
+    if (!count) return hipSuccess;
+    const uint32_t grid = count < 65536u ? count : 65536u;
+    hipLaunchKernelGGL(lzf_clear_tail_kernel, dim3(grid), dim3(256), 0, s, dst, dst_off, len, cap, count);
+    return hipGetLastError();
+}

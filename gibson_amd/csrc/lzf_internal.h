@@ -107,6 +107,10 @@ const char *lzf_compress_kernel_name(void);
  * len[k] (at least min_len) bytes from src + src_off[k] to dst + dst_off[k] */
 hipError_t lzf_launch_move(const uint8_t *src, const uint64_t *src_off, uint8_t *dst, const uint64_t *dst_off,
                            const uint32_t *len, uint32_t min_len, uint32_t count, hipStream_t s);
+/* zero bytes [len[k], cap[k]) of every value's slot at dst + dst_off[k] (the
+ * bytes past a decoded value that a DMA of abutting slots would carry) */
+hipError_t lzf_launch_clear_tail(uint8_t *dst, const uint64_t *dst_off, const uint32_t *len, const uint32_t *cap,
+                                 uint32_t count, hipStream_t s);
 /* lzf_api.cpp, for the host-memory paths of lzf_host.cpp: the routed
  * launches, the routing's batch threshold, the device check, the scratch */
 hipError_t lzf_route_compress(const LzfBatch &b, hipStream_t s);
@@ -121,7 +125,8 @@ hipError_t lzf_route_compress_bulk(const LzfBatch &b, hipStream_t s, void *scrat
  * force (no LZF_GPU_KERNEL override, the LDS lane order held) */
 hipError_t lzf_route_compress_window(const LzfBatch &b, hipStream_t s);
 bool lzf_route_default(void);
-void *lzf_scratch_create(void);
+/* a private scratch holding 1/share of the cap (the host pipeline's slots) */
+void *lzf_scratch_create(unsigned share);
 void lzf_scratch_release(void *scratch);
 void lzf_scratch_destroy(void *scratch);
 const char *lzf_decompress_kernel_name(void);

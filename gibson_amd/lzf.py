@@ -36,6 +36,8 @@ EXPORTS = (
     "lzf_gpu_device_plan",
     "lzf_host_last_spread",
     "lzf_host_split",
+    "lzf_host_split_block",
+    "lzf_host_split_policy",
     "lzf_gpu_parse_device_list",
 )
 
@@ -135,6 +137,10 @@ def _load(path):
     L.lzf_host_last_spread.argtypes = [vp, vp, ctypes.c_int]
     L.lzf_host_split.restype = u32
     L.lzf_host_split.argtypes = [u32, u32, u32, vp, vp]
+    L.lzf_host_split_block.restype = u32
+    L.lzf_host_split_block.argtypes = [u32, u32, u32, vp]
+    L.lzf_host_split_policy.restype = ctypes.c_int
+    L.lzf_host_split_policy.argtypes = []
     L.lzf_gpu_parse_device_list.restype = ctypes.c_int
     L.lzf_gpu_parse_device_list.argtypes = [ctypes.c_char_p, ctypes.c_int, vp, ctypes.c_int]
     del i32
@@ -286,6 +292,19 @@ def host_split(count, groups, g):
     f, s = ctypes.c_uint32(), ctypes.c_uint32()
     n = lib().lzf_host_split(count, groups, g, ctypes.byref(f), ctypes.byref(s))
     return f.value, s.value, n
+
+
+def host_split_block(count, groups, g):
+    """(first, n): the contiguous span entry g of ``groups`` takes under
+    LZF_GPU_SPLIT=block."""
+    f = ctypes.c_uint32()
+    n = lib().lzf_host_split_block(count, groups, g, ctypes.byref(f))
+    return f.value, n
+
+
+def host_split_policy():
+    """"block" when LZF_GPU_SPLIT=block is in force, else "round-robin"."""
+    return "block" if lib().lzf_host_split_policy() == 1 else "round-robin"
 
 
 def parse_device_list(spec, visible):

@@ -128,6 +128,8 @@ int lzf_host_decompress_batch(const uint8_t *in, const uint64_t *in_off, const u
  * failure's code.  Registration costs about 15 ms per GiB (measured).
  */
 int lzf_host_register(const void *ptr, uint64_t len);
+/* (LZF_GPU_ENODEV: some device of the plan gave no device address for the
+ * range; it is then left unregistered.) */
 int lzf_host_unregister(const void *ptr);
 
 /*
@@ -142,8 +144,16 @@ int lzf_gpu_device_plan(int *device, int *numa_node, int *bound, int max);
  * and its wall time in ms (the per-device spread).  Returns G. */
 int lzf_host_last_spread(uint32_t *values, double *ms, int max);
 /* The partition rule: entry g of `groups` takes values first + k * stride,
- * k < the returned count (first = g, stride = groups). */
+ * k < the returned count (first = g, stride = groups): value i to entry
+ * i mod G, the default. */
 uint32_t lzf_host_split(uint32_t count, uint32_t groups, uint32_t g, uint32_t *first, uint32_t *stride);
+/* The contiguous split (LZF_GPU_SPLIT=block): entry g takes the values
+ * [first, first + returned count), first = floor(count * g / groups), so
+ * every entry's share is one span of the caller's arena and its values keep
+ * the registered path's DMA runs. */
+uint32_t lzf_host_split_block(uint32_t count, uint32_t groups, uint32_t g, uint32_t *first);
+/* The split the host-memory calls use: 0 round-robin (default), 1 block. */
+int lzf_host_split_policy(void);
 /* The LZF_GPU_DEVICES grammar ("all", or comma-separated indices below
  * `visible`): fills dev[] and returns the count, or a negative code. */
 int lzf_gpu_parse_device_list(const char *spec, int visible, int *dev, int max);

@@ -181,6 +181,13 @@ DIGEST_CONFIGS = [
 # order of (u32 LE decoded length || the reference decoder's output), the
 # length 0 for a value that did not compress
 ROUNDTRIP = {(0, 0x5EED0004, 8192, 1048576)}
+# round 6: the rest of the configs' real counts, in 1 M-value chunks starting
+# at `first` -- configs[3]'s other 7 M values (with the decoder's output
+# digest) and configs[4]'s other three 1 M chunks
+# (BASELINE config, kind, seed, n, first, count)
+DIGEST_CHUNKS = ([(3, 0, 0x5EED0004, 8192, k << 20, 1 << 20) for k in range(1, 8)] +
+                 [(4, 3, 0x5EED0005, 16384, k << 20, 1 << 20) for k in range(1, 4)])
+ROUNDTRIP_KINDS = {(0, 0x5EED0004, 8192)}
 
 
 def digests(have=()):
@@ -197,10 +204,12 @@ def digests(have=()):
                                         ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     res = []
-    for cfg, kind, seed, n, count in DIGEST_CONFIGS:
-        if (kind, seed, n, count) in have:
-            continue
-        rt = (kind, seed, n, count) in ROUNDTRIP
+    todo = [(cfg, kind, seed, n, 0, count) for cfg, kind, seed, n, count in DIGEST_CONFIGS
+            if (kind, seed, n, count) not in have]
+    todo += [(cfg, kind, seed, n, f0, count) for cfg, kind, seed, n, f0, count in DIGEST_CHUNKS
+             if (kind, seed, n, f0, count) not in have]
+    for cfg, kind, seed, n, f0, count in todo:
+        rt = (kind, seed, n, count) in ROUNDTRIP or (f0 and (kind, seed, n) in ROUNDTRIP_KINDS)
         h, hd = hashlib.sha256(), hashlib.sha256()
         chunk = max(1, min(count, (512 << 20) // n))
         out = np.empty(chunk * n, np.uint8)
@@ -211,10 +220,10 @@ def digests(have=()):
         for first in range(0, count, chunk):
             m = min(chunk, count - first)
             if rt:
-                rc = lib.ref_batch_roundtrip(kind, seed, first, m, n, 4, out.ctypes.data, lens.ctypes.data,
+                rc = lib.ref_batch_roundtrip(kind, seed, f0 + first, m, n, 4, out.ctypes.data, lens.ctypes.data,
                                              dec.ctypes.data, dlens.ctypes.data, os.cpu_count() or 1)
             else:
-                rc = lib.ref_batch_compress(kind, seed, first, m, n, 4, out.ctypes.data, lens.ctypes.data,
+                rc = lib.ref_batch_compress(kind, seed, f0 + first, m, n, 4, out.ctypes.data, lens.ctypes.data,
                                             os.cpu_count() or 1)
             assert rc == 0
             for k in range(m):
@@ -227,13 +236,13 @@ def digests(have=()):
                     hd.update(dl.to_bytes(4, "little"))
                     hd.update(dec[k * n:k * n + dl].data)
             total += m
-        rec = {"config": cfg, "kind": kind, "seed": seed, "n": n, "first": 0, "count": count,
+        rec = {"config": cfg, "kind": kind, "seed": seed, "n": n, "first": f0, "count": count,
                "out_len": "n-4", "sha256": h.hexdigest(), "comp_bytes": comp}
         if rt:
             rec["decoded_sha256"] = hd.hexdigest()
             rec["decode_out_len"] = "n"
         res.append(rec)
-        print("digest", cfg, n, count, h.hexdigest()[:16], comp / (count * n))
+        print("digest", cfg, n, f0, count, h.hexdigest()[:16], comp / (count * n), flush=True)
     return res
 
 
@@ -268,7 +277,8 @@ def main():
         path = os.path.join(here, "digests.json")
         with open(path) as f:
             doc = json.load(f)
-        have = {(d["kind"], d["seed"], d["n"], d["count"]) for d in doc["digests"]}
+        have = {(d["kind"], d["seed"], d["n"], d["count"]) for d in doc["digests"] if not d.get("first")}
+        have |= {(d["kind"], d["seed"], d["n"], d["first"], d["count"]) for d in doc["digests"] if d.get("first")}
         doc["digests"] += digests(have)
         with open(path, "w") as f:
             json.dump(doc, f, indent=1)

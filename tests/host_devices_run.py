@@ -94,7 +94,7 @@ def digest_case(register):
 
 def main():
     oracle = Oracle()
-    res = {"plan": gibson_amd.device_plan()}
+    res = {"plan": gibson_amd.device_plan(), "split": gibson_amd.host_split_policy()}
     for reg in (False, True):
         tag = "registered" if reg else "staged"
         res["mixed_" + tag] = mixed_case(oracle, reg)

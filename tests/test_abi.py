@@ -65,7 +65,7 @@ ROUTED = {"lzf_cand_stream_kernel", "lzf_parse_lane_kernel", "lzf_cand_table_ker
           "lzf_compress_window_kernel", "lzf_decompress_pipe_kernel", "lzf_decompress_tokpar_kernel",
           "lzf_dsize_kernel", "lzf_lds_order_probe_kernel", "lzf_synth_kernel", "lzf_frame_size_kernel",
           "lzf_frame_scan_kernel", "lzf_frame_write_kernel", "lzf_frame_check_kernel",
-          "lzf_move_kernel"}
+          "lzf_move_kernel", "lzf_clear_tail_kernel"}
 # cross-check forms: the diagnostic build only
 DIAG_ONLY = {"lzf_wparse_kernel", "lzf_cand_q1_kernel", "lzf_cand_small_kernel", "lzf_cand_ring_kernel",
              "lzf_cand_mid_kernel", "lzf_compress_serial_kernel", "lzf_decompress_serial_kernel",

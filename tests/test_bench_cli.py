@@ -35,6 +35,56 @@ def test_bench_small_run(args):
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["config"]["roundtrip_ok"] is True
     assert line["value"] > 0 and line["roofline"]["peak"] == 8000.0
+    if "--mode" not in args:
+        assert 0 < line["roofline"]["roundtrip_frac"] < 1
+
+
+def _args(argv):
+    sys.path.insert(0, ROOT)
+    import bench
+    old = sys.argv
+    sys.argv = ["bench.py"] + argv
+    try:
+        return bench, bench.parse()
+    finally:
+        sys.argv = old
+
+
+@pytest.mark.parametrize("argv,world,want", [
+    ([], 1, False),                                   # the driver's N = 1 line: configs[2] only
+    ([], 2, True),                                    # the driver's N > 1 lines: + configs[4]
+    ([], 8, True),
+    (["--no-config4"], 8, False),
+    (["--workload", "text64k"], 8, False),            # an explicit workload is measured alone
+    (["--workload", "mixed16k", "--total", "4194304"], 8, False),
+    (["--count", "4096"], 2, False),
+    (["--config4"], 1, True),
+    (["--mode", "decompress"], 8, False),
+])
+def test_config4_block_choice(argv, world, want):
+    # N > 1 on the default workload keeps `value` on configs[2] (weak
+    # scaling: the driver's 1 -> 8 curve compares like with like) and adds
+    # the configs[4] strong split, the config the >= 0.9x per-GPU efficiency
+    # target is stated on, as a config4 block
+    bench, a = _args(argv)
+    assert bench.wants_config4(a, world) is want
+    assert a.config4_total == 4194304
+
+
+def test_config4_block_efficiency_against_committed_n1(tmp_path, monkeypatch):
+    bench, _ = _args([])
+    import json
+    f = tmp_path / "n1.json"
+    f.write_text(json.dumps({"value": 80.0, "total_values": 4194304}))
+    monkeypatch.setattr(bench, "CONFIG4_N1", str(f))
+    r4 = {"wall": 2.0, "steps": 4, "in_bytes_all": 4194304 * 16384, "bad_ranks": 0, "nch": 1,
+          "t_comp": 0.4, "t_dec": 0.05}
+    blk = bench.config4_block(8, r4, 4194304, 16384)
+    assert blk["baseline_config"] == 4 and blk["roundtrip_ok"] is True
+    assert abs(blk["value"] - 4194304 * 16384 / 0.5 / 1e9) < 1e-3
+    assert blk["per_gpu_efficiency"] == round(blk["value"] / (8 * 80.0), 4)
+    # a different total is not compared with the committed figure
+    assert bench.config4_block(8, r4, 65536, 16384)["per_gpu_efficiency"] is None
 
 
 def test_bench_gpus_must_match_world_size():
@@ -72,6 +122,7 @@ def test_bench_default_is_configs2_with_cpu_baseline():
 @pytest.mark.parametrize("args", [
     ["--count", "4096"],                                          # weak scaling, round trip
     ["--workload", "mixed16k", "--total", "8192"],                # strong scaling (configs[4] shape)
+    ["--count", "4096", "--config4", "--config4-total", "16384"],  # + the configs[4] block
 ])
 def test_bench_two_ranks_rehearsal(args):
     # the N-rank path end to end on one GPU: --gpus 2 starts two ranks as a
@@ -92,3 +143,9 @@ def test_bench_two_ranks_rehearsal(args):
     assert line["scaling"] == ("strong" if "--total" in args else "weak")
     if "--total" in args:
         assert line["config"]["values_per_gpu"] == 4096
+    assert 0 < line["roofline"]["roundtrip_frac"] < 1
+    if "--config4" in args:
+        c4 = line["config4"]
+        assert c4["baseline_config"] == 4 and c4["roundtrip_ok"] is True
+        assert c4["total_values"] == 16384 and c4["values_per_gpu_max"] == 8192
+        assert c4["per_gpu_efficiency"] is None          # not the committed N = 1 configuration

@@ -562,7 +562,8 @@ CONFIGS = [
 def digests():
     import json
     with open(os.path.join(os.path.dirname(__file__), "golden", "digests.json")) as f:
-        return {(d["kind"], d["seed"], d["n"], d["count"]): d["sha256"] for d in json.load(f)["digests"]}
+        return {(d["kind"], d["seed"], d["n"], d["count"]): d["sha256"] for d in json.load(f)["digests"]
+                if not d.get("first")}
 
 
 @pytest.mark.parametrize("kind,seed,n,count", CONFIGS)
@@ -607,8 +608,27 @@ def test_full_count_digest(kind, seed, n, count, digests, monkeypatch):
     import json
     monkeypatch.delenv("LZF_GPU_LANE_MIN", raising=False)
     with open(os.path.join(os.path.dirname(__file__), "golden", "digests.json")) as f:
-        rec = {(d["kind"], d["seed"], d["n"], d["count"]): d for d in json.load(f)["digests"]}
+        rec = {(d["kind"], d["seed"], d["n"], d["count"]): d for d in json.load(f)["digests"] if not d.get("first")}
     _digest_case(kind, seed, n, count, digests, decoded=rec[(kind, seed, n, count)].get("decoded_sha256"))
+
+
+# round 6: the rest of the configs' real counts, one 1 M-value chunk per test
+# -- configs[3]'s values 1 M .. 8 M (streams and the reference decoder's
+# output), configs[4]'s values 1 M .. 4 M -- so every value of configs[1],
+# [3] and [4] and all of configs[2] is checked against the reference
+CHUNKS = [(0, 0x5EED0004, 8192, k << 20) for k in range(1, 8)] + [(3, 0x5EED0005, 16384, k << 20) for k in range(1, 4)]
+
+
+@pytest.mark.parametrize("kind,seed,n,first", CHUNKS, ids=[f"k{c[0]}-{c[2]}-{c[3] >> 20}M" for c in CHUNKS])
+def test_full_count_digest_chunk(kind, seed, n, first, monkeypatch):
+    import json
+    monkeypatch.delenv("LZF_GPU_LANE_MIN", raising=False)
+    count = 1 << 20
+    with open(os.path.join(os.path.dirname(__file__), "golden", "digests.json")) as f:
+        rec = {(d["kind"], d["seed"], d["n"], d.get("first", 0), d["count"]): d for d in json.load(f)["digests"]}
+    r = rec[(kind, seed, n, first, count)]
+    _digest_case(kind, seed, n, count, {(kind, seed, n, count): r["sha256"]}, decoded=r.get("decoded_sha256"),
+                 first=first)
 
 
 @pytest.mark.parametrize("gen,chunks", [("default", 3), ("table", 5)])
@@ -625,12 +645,12 @@ def test_full_batch_digest_chunked_scratch(digests, monkeypatch, gen, chunks):
     assert _chunks() == chunks, _chunks()
 
 
-def _digest_case(kind, seed, n, count, digests, decoded=None):
+def _digest_case(kind, seed, n, count, digests, decoded=None, first=0):
     import gibson_amd
     from tests.digest import batch_digest
     dev = "cuda"
     src = torch.empty(count * n, dtype=torch.uint8, device=dev)
-    gibson_amd.synth_fill(kind, seed, 0, 1, count, n, src)
+    gibson_amd.synth_fill(kind, seed, first, 1, count, n, src)
     in_off = torch.arange(count, dtype=torch.int64, device=dev) * n
     in_len = torch.full((count,), n, dtype=torch.int32, device=dev)
     cap = torch.full((count,), n - 4, dtype=torch.int32, device=dev)

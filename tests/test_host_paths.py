@@ -174,16 +174,19 @@ def test_register_rejects_overlap():
         gibson_amd.host_unregister(a)
 
 
-def test_two_contexts_on_one_device_bit_exact(digests_full):
-    # LZF_GPU_DEVICES=0,0: the round-robin split over two worker contexts,
-    # staged and registered, against the oracle and configs[1]'s digest
-    env = dict(os.environ, LZF_GPU_DEVICES="0,0")
+@pytest.mark.parametrize("split", ["rr", "block"])
+def test_two_contexts_on_one_device_bit_exact(digests_full, split):
+    # LZF_GPU_DEVICES=0,0: the round-robin split (default) or the contiguous
+    # one (LZF_GPU_SPLIT=block) over two worker contexts, staged and
+    # registered, against the oracle and configs[1]'s digest
+    env = dict(os.environ, LZF_GPU_DEVICES="0,0", LZF_GPU_SPLIT=split)
     env.pop("LZF_GPU_LANE_MIN", None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "host_devices_run.py")], env=env,
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert [p[0] for p in res["plan"]] == [0, 0]
+    assert res["split"] == ("block" if split == "block" else "round-robin")
     want = digests_full[(1, 0x5EED0002, 4096, 262144)]
     for tag in ("staged", "registered"):
         m = res["mixed_" + tag]
@@ -197,7 +200,8 @@ def test_two_contexts_on_one_device_bit_exact(digests_full):
 @pytest.fixture(scope="module")
 def digests_full():
     with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
-        return {(d["kind"], d["seed"], d["n"], d["count"]): d["sha256"] for d in json.load(f)["digests"]}
+        return {(d["kind"], d["seed"], d["n"], d["count"]): d["sha256"] for d in json.load(f)["digests"]
+                if not d.get("first")}
 
 
 def test_registered_bulk_chunks_config1_digest(digests_full, registered):
@@ -235,16 +239,22 @@ def test_bad_device_plan_is_reported_not_aborted():
     assert r.stdout.split() == ["-3", "-3"], r.stdout
 
 
-@pytest.mark.parametrize("share,chunks", [(None, None), (50, 4)], ids=["default", "50pct-4chunks"])
-def test_registered_tail_mode_64k(oracle, registered, monkeypatch, share, chunks):
+@pytest.mark.parametrize("share,chunks,cap_mb", [(None, None, None), (50, 4, None), (None, None, 64), (None, None, 24)],
+                         ids=["default", "50pct-4chunks", "cap64MiB", "cap24MiB-slot-reuse"])
+def test_registered_tail_mode_64k(oracle, registered, monkeypatch, share, chunks, cap_mb):
     # 256 MiB of 64 KiB values (configs[2]'s generator): the registered path's
     # tail mode -- the first part of the values through the table generation,
     # the rest by window64 in chunks beside its parse (default 70 % and one
-    # chunk; 50 % and four, each chunk in its own slot) -- against the staged
-    # path and a sample of the oracle that includes every chunk boundary
+    # chunk; 50 % and four, each chunk in its own slot; under a chunk cap
+    # (LZF_GPU_HOST_CHUNK_MB) both parts split into chunks of at most the cap:
+    # 64 MiB gives 3 + 2 chunks, 24 MiB 8 + 4, more chunks than slots) --
+    # against the staged path and a sample of the oracle that includes every
+    # chunk boundary
     if share is not None:
         monkeypatch.setenv("LZF_GPU_HOST_TAIL", str(share))
         monkeypatch.setenv("LZF_GPU_HOST_TAIL_CHUNKS", str(chunks))
+    if cap_mb is not None:
+        monkeypatch.setenv("LZF_GPU_HOST_CHUNK_MB", str(cap_mb))
     import gibson_amd
     from tests.oracle_lib import _SYN
     n, count = 65536, 4096
@@ -265,6 +275,11 @@ def test_registered_tail_mode_64k(oracle, registered, monkeypatch, share, chunks
     pct, nch = (share or 70), (chunks or 1)
     t = count * pct // 100
     edges = [t + (count - t) * k // nch for k in range(nch)]
+    if cap_mb is not None:                       # the capped plan's chunk edges (equal bytes: equal counts here)
+        per = (cap_mb << 20) // n
+        r = -(-t // per)
+        q = max(nch, -(-(count - t) // per))
+        edges += [t * k // r for k in range(r)] + [t + (count - t) * k // q for k in range(q)]
     for i in sorted(set(list(range(0, count, 97)) + [e + d for e in edges for d in (-1, 0)] + [count - 1])):
         exp = oracle.compress(bytes(arena[i * n:(i + 1) * n]), n - 4)
         assert bytes(out_r[i * n:i * n + olen_r[i]]) == exp, i
@@ -321,3 +336,60 @@ def test_registered_bulk_mixed_sizes(oracle, registered, monkeypatch, env):
     assert (dl == ln[ok]).all() and (er == 0).all()
     for i in np.nonzero(ok)[0]:
         assert bytes(dec[offs[i]:offs[i] + sizes[i]]) == bytes(arena[offs[i]:offs[i] + sizes[i]]), i
+
+
+def test_register_refused_unless_every_plan_device_maps(monkeypatch):
+    # lzf_host_register asks every distinct device of the plan for the
+    # range's device address (first and last byte); a device that gives none
+    # (forced here for device 0) makes the registration fail whole: ENODEV,
+    # the range left unregistered, and it registers normally afterwards
+    import gibson_amd
+    a = _aligned(1 << 20)
+    monkeypatch.setenv("LZF_GPU_FORCE_MAP_FAIL", "0")
+    with pytest.raises(RuntimeError, match="ENODEV"):
+        gibson_amd.host_register(a)
+    monkeypatch.delenv("LZF_GPU_FORCE_MAP_FAIL")
+    gibson_amd.host_register(a)
+    gibson_amd.host_unregister(a)
+
+
+def test_registered_decode_leaves_no_stale_bytes(oracle, registered):
+    # abutting output slots go back to the caller as DMA runs of whole slots:
+    # a second batch into the same layout whose streams decode short or fail
+    # must not carry the first batch's decoded bytes past its own out_len
+    # (they are zeroed on the device first)
+    import gibson_amd
+    count, n = 512, 4096
+    vals = [synth(k % 6, 0x5EED00B7, k, n) for k in range(count)]
+    streams = [oracle.compress(v, n + 64) for v in vals]
+    pos, offs = 0, []
+    for st in streams:
+        offs.append(pos)
+        pos += len(st)
+    inp = registered(_aligned(pos + 16))
+    for st, o in zip(streams, offs):
+        inp[o:o + len(st)] = np.frombuffer(st, np.uint8)
+    out = registered(_aligned(count * n))
+    doff = np.arange(count, dtype=np.uint64) * n
+    dl = np.zeros(count, np.uint32)
+    er = np.zeros(count, np.int32)
+    ioff = np.array(offs, np.uint64)
+    ilen = np.array([len(st) for st in streams], np.uint32)
+    gibson_amd.host_decompress_batch(inp, ioff, ilen, out, doff, np.full(count, n, np.uint32), dl, er)
+    assert (dl == n).all() and bytes(out[:n]) == vals[0]
+    # the same slots again: every third stream truncated (fails), every third
+    # other one decoded into a cap of half its length (E2BIG)
+    cut = ilen.copy()
+    cut[0::3] = np.maximum(cut[0::3] // 2, 1)
+    caps = np.full(count, n, np.uint32)
+    caps[1::3] = n // 2
+    out[:] = 0xA5
+    gibson_amd.host_decompress_batch(inp, ioff, cut, out, doff, caps, dl, er)
+    for k in range(count):
+        e = oracle.decompress(bytes(inp[offs[k]:offs[k] + cut[k]]), int(caps[k]))
+        s = out[k * n:(k + 1) * n]
+        if e[0] is None:
+            assert dl[k] == 0 and er[k] == e[1], k
+        else:
+            assert bytes(s[:dl[k]]) == e[0], k
+        assert not (s[dl[k]:caps[k]] != 0).any(), k         # no stale device bytes

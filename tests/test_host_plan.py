@@ -26,6 +26,37 @@ def test_split_outside_the_plan_is_empty():
     assert gibson_amd.host_split(3, 8, 5)[2] == 0
 
 
+@pytest.mark.parametrize("count", [0, 1, 2, 3, 7, 8, 9, 1000, 262144, 262147, 4194304])
+@pytest.mark.parametrize("groups", [1, 2, 3, 8])
+def test_split_block_is_contiguous(count, groups):
+    # LZF_GPU_SPLIT=block: entry g takes [floor(count g / G), floor(count (g+1) / G)),
+    # the spans abut in entry order and cover the batch once; sizes differ by
+    # at most one value
+    end, sizes = 0, []
+    for g in range(groups):
+        first, n = gibson_amd.host_split_block(count, groups, g)
+        assert first == count * g // groups == end
+        assert n == count * (g + 1) // groups - first
+        end = first + n
+        sizes.append(n)
+    assert end == count
+    assert max(sizes) - min(sizes) <= 1
+
+
+def test_split_block_outside_the_plan_is_empty():
+    assert gibson_amd.host_split_block(10, 4, 4)[1] == 0
+    assert gibson_amd.host_split_block(10, 0, 0)[1] == 0
+
+
+@pytest.mark.parametrize("env,want", [(None, "round-robin"), ("rr", "round-robin"), ("block", "block")])
+def test_split_policy_from_env(env, want, monkeypatch):
+    if env is None:
+        monkeypatch.delenv("LZF_GPU_SPLIT", raising=False)
+    else:
+        monkeypatch.setenv("LZF_GPU_SPLIT", env)
+    assert gibson_amd.host_split_policy() == want
+
+
 def test_gather_order_restores_the_batch():
     # a stand-in for the workers: each entry "processes" its share in its own
     # order and writes result i at index i -- the caller's array comes back whole

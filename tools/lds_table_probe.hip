@@ -29,7 +29,7 @@ __device__ __forceinline__ unsigned lds_addr(const void *p)
 #define P5(i) "ds_read_u16 %" #i ", %[h" #i "]\n\tds_write_b16 %[h" #i "], %[d" #i "]\n\t"
 
 template <int MODE>
-__global__ __launch_bounds__(256) void tk(unsigned long long *cyc, unsigned *sink, int iters, int dup)
+__global__ __launch_bounds__(256) void tk(unsigned long long *cyc, unsigned *sink, int iters, int dup, int dense)
 {
     __shared__ __attribute__((aligned(16))) unsigned short T[65536 + 64];
     const unsigned lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -67,7 +67,10 @@ __global__ __launch_bounds__(256) void tk(unsigned long long *cyc, unsigned *sin
 #pragma unroll
                 for (unsigned u = 0; u < 5u; u++) {
                     r[u] = 0u;
-                    if ((h[u] >> 2) % nw == wv)
+                    /* dense: whole windows dealt to the waves (the compacted
+                     * slot-partition packets of a split table role); else
+                     * every wave issues every window, exec-masked by slot */
+                    if (dense ? ((g + u) % nw == wv) : ((h[u] >> 2) % nw == wv))
                         asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3" : "=&v"(r[u]) : "v"(a[u]), "v"(m[u]), "v"(d[u]) : "memory");
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]) :: "memory");
@@ -146,10 +149,10 @@ int main()
     for (int dup = 0; dup < 2; dup++)
         for (int mode = 0; mode < 4; mode++) {
             for (int rep = 0; rep < 2; rep++) {
-                if (mode == 0) hipLaunchKernelGGL(tk<0>, dim3(cus), dim3(64), 0, 0, dc, ds, iters, dup);
-                if (mode == 1) hipLaunchKernelGGL(tk<1>, dim3(cus), dim3(64), 0, 0, dc, ds, iters, dup);
-                if (mode == 2) hipLaunchKernelGGL(tk<2>, dim3(cus), dim3(64), 0, 0, dc, ds, iters, dup);
-                if (mode == 3) hipLaunchKernelGGL(tk<3>, dim3(cus), dim3(64), 0, 0, dc, ds, iters, dup);
+                if (mode == 0) hipLaunchKernelGGL(tk<0>, dim3(cus), dim3(64), 0, 0, dc, ds, iters, dup, 0);
+                if (mode == 1) hipLaunchKernelGGL(tk<1>, dim3(cus), dim3(64), 0, 0, dc, ds, iters, dup, 0);
+                if (mode == 2) hipLaunchKernelGGL(tk<2>, dim3(cus), dim3(64), 0, 0, dc, ds, iters, dup, 0);
+                if (mode == 3) hipLaunchKernelGGL(tk<3>, dim3(cus), dim3(64), 0, 0, dc, ds, iters, dup, 0);
                 hipDeviceSynchronize();
             }
             hipMemcpy(hc, dc, sizeof(unsigned long long) * cus, hipMemcpyDeviceToHost);
@@ -159,17 +162,19 @@ int main()
             printf("%-22s dup=%d: %8.1f memtime ticks per window (%.0f shader cycles at 2.4 GHz)\n", nm[mode], dup,
                    s / cus / iters / 15.0, s / cus / iters / 15.0 * 24.0);
         }
+    for (int dense = 0; dense < 2; dense++)
     for (int dup = 0; dup < 2; dup++)
         for (int nw = 1; nw <= 4; nw *= 2) {
             for (int rep = 0; rep < 2; rep++) {
-                hipLaunchKernelGGL(tk<0>, dim3(cus), dim3(64 * nw), 0, 0, dc, ds, iters, dup);
+                hipLaunchKernelGGL(tk<0>, dim3(cus), dim3(64 * nw), 0, 0, dc, ds, iters, dup, dense);
                 hipDeviceSynchronize();
             }
             hipMemcpy(hc, dc, sizeof(unsigned long long) * cus, hipMemcpyDeviceToHost);
             double s = 0;
             for (int i = 0; i < cus; i++) s += (double)hc[i];
-            printf("exchange split over %d waves (by slot, exec-masked) dup=%d: %8.1f cycles per window\n", nw, dup,
-                   s / cus / iters / 15.0);
+            /* per window of the whole step: 15 windows per step whatever nw */
+            printf("exchange split over %d waves (%s) dup=%d: %8.1f shader cycles per window of the step\n", nw,
+                   dense ? "dense windows dealt per wave" : "by slot, exec-masked", dup, s / cus / iters / 15.0 * 24.0);
         }
     unsigned bad = 0, tot = 0;
     for (int ng = 1; ng <= 64; ng *= 2) {
