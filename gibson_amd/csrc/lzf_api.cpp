@@ -201,7 +201,8 @@ thread_local uint32_t g_last_chunks = 0;
 
 /* own: a caller's private scratch (the host pipelines' slots, so their
  * chunks' compress launches can run side by side), else the device's */
-hipError_t lane_compress(const LzfBatch &b, hipStream_t s, ScratchUser who, Scratch *own = nullptr)
+hipError_t lane_compress(const LzfBatch &b, hipStream_t s, ScratchUser who, Scratch *own = nullptr,
+                         const LzfParts *parts = nullptr)
 {
     const bool table = who == SU_TABLE;
     int dev = 0;
@@ -244,7 +245,7 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s, ScratchUser who, Scra
      * when one is set below it */
     const size_t use = capped && lim < S.cap ? (lim > 2 * per + 1024 ? lim : 2 * per + 1024) : S.cap;
     if (table) {
-        e = lzf_launch_compress_table(b, s, S.p, use, &g_last_chunks);
+        e = lzf_launch_compress_table(b, s, S.p, use, &g_last_chunks, parts);
     }
 #ifdef LZF_DIAG
     else if (who == SU_WTAB) {
@@ -252,6 +253,9 @@ hipError_t lane_compress(const LzfBatch &b, hipStream_t s, ScratchUser who, Scra
     }
 #endif
     else {
+        /* the lane generation takes the batch whole: every part in first */
+        for (uint32_t p = 0; parts && p < parts->n; p++)
+            if ((e = hipStreamWaitEvent(s, parts->ev[p], 0)) != hipSuccess) return e;
 #ifdef LZF_DIAG
         const char *ff = getenv("LZF_GPU_LANE_FORCE_FIX");
         /* LZF_GPU_LANE_PIPE=1 overlaps the two kernels of consecutive chunks
@@ -298,9 +302,18 @@ uint32_t lane_min_count(uint32_t max_len)
 /* bulk: the caller runs several launches side by side (the host-memory
  * pipeline), so the per-launch floor of the parse overlaps and the batch
  * threshold below which window64 wins alone does not apply */
-hipError_t launch_compress(const LzfBatch &b, hipStream_t s, Scratch *own = nullptr, bool bulk = false)
+hipError_t launch_compress(const LzfBatch &b, hipStream_t s, Scratch *own = nullptr, bool bulk = false,
+                           const LzfParts *parts = nullptr)
 {
     const KernelGen g = kernel_gen();
+    /* inputs in parts: a route that takes the batch whole waits for all */
+    const bool routed_default = g == GEN_TABLE && lds_order_ok() && lzf_table_compress_supported(b.max_len);
+    if (parts && !routed_default)
+        for (uint32_t p = 0; p < parts->n; p++) {
+            const hipError_t e = hipStreamWaitEvent(s, parts->ev[p], 0);
+            if (e != hipSuccess) return e;
+        }
+    if (!routed_default) parts = nullptr;
     if (g != GEN_WINDOW && g != GEN_SERIAL && !lds_order_ok()) return lzf_launch_compress(b, s);
     switch (g) {
 #ifdef LZF_DIAG
@@ -327,8 +340,13 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s, Scratch *own = null
          * most LANE_DEFAULT_MAX bytes take the lane generation (the stream
          * cand kernel, lzf_stream.hip, and the lane parse), larger ones the
          * table generation (two-link records, lzf_cand.hip) */
-        if ((!bulk && b.count < lane_min_count(b.max_len)) || !lzf_table_compress_supported(b.max_len))
+        if ((!bulk && b.count < lane_min_count(b.max_len)) || !lzf_table_compress_supported(b.max_len)) {
+            for (uint32_t p = 0; parts && p < parts->n; p++) {
+                const hipError_t e = hipStreamWaitEvent(s, parts->ev[p], 0);
+                if (e != hipSuccess) return e;
+            }
             return lzf_launch_compress(b, s);
+        }
         /* the lane generation where its kernel 1 takes the batch (a
          * diagnostic LZF_GPU_CAND=small stops at 4 KiB), else the table one --
          * unless the scratch cap splits the table generation into more chunks
@@ -357,7 +375,7 @@ hipError_t launch_compress(const LzfBatch &b, hipStream_t s, Scratch *own = null
                     lane = (need_t + lim - 1) / lim > (need_l + lim - 1) / lim;
                 }
             }
-            return lane_compress(b, s, lane ? SU_LANE : SU_TABLE, own);
+            return lane_compress(b, s, lane ? SU_LANE : SU_TABLE, own, parts);
         }
     }
 }
@@ -404,9 +422,9 @@ uint32_t lzf_route_min_count(uint32_t max_len) { return lane_min_count(max_len);
 bool lzf_device_ok(int dev) { return device_ok(dev); }
 hipError_t lzf_route_compress_window(const LzfBatch &b, hipStream_t s) { return lzf_launch_compress(b, s); }
 bool lzf_route_default(void) { return kernel_gen() == GEN_TABLE && lds_order_ok(); }
-hipError_t lzf_route_compress_bulk(const LzfBatch &b, hipStream_t s, void *scratch)
+hipError_t lzf_route_compress_bulk(const LzfBatch &b, hipStream_t s, void *scratch, const LzfParts *parts)
 {
-    return launch_compress(b, s, (Scratch *)scratch, true);
+    return launch_compress(b, s, (Scratch *)scratch, true, parts);
 }
 void *lzf_scratch_create(unsigned share)
 {

@@ -1077,7 +1077,7 @@ size_t lzf_table_scratch_per_value(uint32_t max_len)
 bool lzf_table_compress_supported(uint32_t max_len) { return max_len <= LZF_SLOTS; }
 
 hipError_t lzf_launch_compress_table(const LzfBatch &b, hipStream_t s, void *scratch, size_t scratch_bytes,
-                                     uint32_t *chunks)
+                                     uint32_t *chunks, const LzfParts *parts)
 {
     if (b.max_len > LZF_SLOTS) return hipErrorInvalidValue;
     const uint64_t rstride = rec_stride(b.max_len), bstride = rec_bstride(b.max_len);
@@ -1110,6 +1110,38 @@ hipError_t lzf_launch_compress_table(const LzfBatch &b, hipStream_t s, void *scr
         cus = 256;
     hipError_t e;
     if (chunks) *chunks = (uint32_t)((b.count + chunk - 1u) / chunk);
+    if (parts && parts->n) {
+        if (chunk < b.count || stream || cand_only || parts->end[parts->n - 1u] != b.count) {
+            /* not one chunk: every part in first, then the plain launch */
+            for (uint32_t p = 0; p < parts->n; p++)
+                if ((e = hipStreamWaitEvent(s, parts->ev[p], 0)) != hipSuccess) return e;
+        } else {
+            /* kernel 1 per part as its inputs arrive (its records go to the
+             * part's own rows of the scratch), then one parse over the batch */
+            uint32_t lo = 0;
+            for (uint32_t p = 0; p < parts->n; p++) {
+                const uint32_t hi = parts->end[p];
+                if ((e = hipStreamWaitEvent(s, parts->ev[p], 0)) != hipSuccess) return e;
+                if (hi <= lo) continue;
+                LzfBatch c = b;
+                c.in_off = b.in_off + lo;
+                c.in_len = b.in_len + lo;
+                c.out_off = b.out_off + lo;
+                c.out_cap = b.out_cap + lo;
+                c.out_len = b.out_len + lo;
+                c.count = hi - lo;
+                LzfRecScratch sp = sc;
+                sp.rec = sc.rec + (uint64_t)lo * rstride;
+                const uint32_t g = c.count < (uint32_t)cus ? c.count : (uint32_t)cus;
+                hipLaunchKernelGGL(lzf_cand_table_kernel, dim3(g), dim3(KT_THREADS), 0, s, c, sp);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+                lo = hi;
+            }
+            hipLaunchKernelGGL(lzf_parse_rec_kernel, dim3((b.count + K3_THREADS - 1u) / K3_THREADS),
+                               dim3(K3_THREADS), 0, s, b, sc);
+            return hipGetLastError();
+        }
+    }
     for (uint64_t first = 0; first < b.count; first += chunk) {
         const uint32_t cnt = (uint32_t)((b.count - first) < chunk ? (b.count - first) : chunk);
         LzfBatch c = b;

@@ -259,6 +259,11 @@ struct Ctx {
     bool numa_bound = false;
     hipStream_t stream = nullptr;
     Buf d_in, d_out, d_meta;
+    /* registered decode: the whole batch's input span, copied ahead of the
+     * chunks on its own stream (one event per chunk's part) */
+    Buf d_span;
+    hipStream_t in_stream = nullptr;
+    std::vector<hipEvent_t> in_ev;
     Buf h_in{nullptr, 0, true}, h_out{nullptr, 0, true}, h_meta{nullptr, 0, true};
     Slot slot[NSLOT_ALL];
     Ctx(int device, bool bound) : dev(device), numa_bound(bound)
@@ -293,7 +298,8 @@ struct Ctx {
             lzf_scratch_release(sl.scratch);
             sl.busy = false;
         }
-        for (Buf *b : {&d_in, &d_out, &d_meta, &h_in, &h_out, &h_meta}) b->release();
+        if (in_stream) (void)hipStreamSynchronize(in_stream);
+        for (Buf *b : {&d_in, &d_out, &d_meta, &h_in, &h_out, &h_meta, &d_span}) b->release();
         if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
     }
     /* after a failure: wait for what is in flight, so the buffers are free */
@@ -301,6 +307,7 @@ struct Ctx {
     {
         if (!ok) return;
         if (stream) (void)hipStreamSynchronize(stream);
+        if (in_stream) (void)hipStreamSynchronize(in_stream);
         for (auto &sl : slot) {
             if (sl.stream) (void)hipStreamSynchronize(sl.stream);
             sl.busy = false;
@@ -311,6 +318,8 @@ struct Ctx {
     {
         release();
         for (auto &sl : slot) lzf_scratch_destroy(sl.scratch);
+        for (hipEvent_t e : in_ev) (void)hipEventDestroy(e);
+        if (in_stream) (void)hipStreamDestroy(in_stream);
     }
 };
 
@@ -729,6 +738,55 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
     }
     const uint32_t min_len = a.compress ? 0u : 1u;
 
+    /* Decode, several chunks: the inputs of the whole batch go H2D ahead of
+     * the chunks, one DMA piece per chunk on the context's input stream, so
+     * the compressed bytes cross the bus at once instead of one chunk per
+     * slot turn; each chunk's kernels wait for their piece only.  The D2H
+     * side then carries the decoded bytes alone once the (smaller) inputs
+     * are in.  Taken when the inputs' whole span, gaps included, is no
+     * larger than the outputs (as the per-chunk span below) and fits
+     * LZF_GPU_HOST_SPAN_MB (default 8192). */
+    uint8_t *d_all = nullptr;
+    uint64_t alo = ~0ull, ahi = 0, apad = 0;
+    if (!a.compress && bound.size() > 2) {
+        uint64_t outb = 0;
+        for (uint32_t k = 0; k < v.count; k++) {
+            const uint32_t i = v.at(k);
+            const uint64_t so = a.in_off[i], ext = in_extent(a, i);
+            if (so < alo) alo = so;
+            if (so + ext > ahi) ahi = so + ext;
+            outb += a.out_cap[i];
+        }
+        uint64_t span_cap = 8192ull << 20;
+        if (const char *e = getenv("LZF_GPU_HOST_SPAN_MB")) span_cap = (uint64_t)strtoull(e, nullptr, 10) << 20;
+        if (ahi > alo && ahi - alo <= outb && ahi - alo <= span_cap) {
+            apad = ((uintptr_t)in_map + alo) & 15u;
+            d_all = (uint8_t *)c.d_span.get(ahi - alo + apad + 16);
+            if (!c.in_stream) check(hipStreamCreateWithFlags(&c.in_stream, hipStreamNonBlocking), "hipStreamCreate");
+            while (c.in_ev.size() < bound.size()) {
+                hipEvent_t ev;
+                check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+                c.in_ev.push_back(ev);
+            }
+            /* the span in chunk order: piece r ends where chunk r's inputs end */
+            uint64_t done = alo;
+            for (uint32_t r = 0; r + 1 < bound.size(); r++) {
+                uint64_t hi = done;
+                for (uint32_t k = bound[r]; k < bound[r + 1]; k++) {
+                    const uint32_t i = v.at(k);
+                    const uint64_t e = a.in_off[i] + in_extent(a, i);
+                    if (e > hi) hi = e;
+                }
+                if (hi > done)
+                    check(hipMemcpyAsync(d_all + apad + (done - alo), a.in + done, hi - done, hipMemcpyHostToDevice,
+                                         c.in_stream),
+                          "hipMemcpyAsync");
+                check(hipEventRecord(c.in_ev[r], c.in_stream), "hipEventRecord");
+                done = hi;
+            }
+        }
+    }
+
     auto drain = [&](Slot &sl) {
         if (!sl.busy) return;
         check(hipEventSynchronize(sl.done), "hipEventSynchronize");
@@ -746,6 +804,8 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         uint64_t host, dev, len;
     };
     std::vector<Run> iruns, oruns;
+    std::vector<uint32_t> run_part;          /* the input part of each input run (cand parts) */
+    std::vector<uint32_t> part_end;
     uint32_t round = 0;
     for (; round + 1 < bound.size(); round++) {
         const uint32_t k0 = bound[round], n = bound[round + 1] - k0;
@@ -771,6 +831,21 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
          * slots. */
         iruns.clear();
         oruns.clear();
+        /* Tail mode's routed chunk(s), inputs moved by DMA runs: the runs go
+         * over the bus in LZF_GPU_HOST_CAND_PARTS parts (default 4) on the
+         * context's input stream, and the table generation's kernel 1 runs
+         * each part as it arrives, so the parse -- the per-value chain --
+         * starts right after the last part instead of after a whole cand. */
+        uint32_t nparts = 0;
+        if (a.compress && bulk && k0 < tail_from && tail_from < v.count) {
+            nparts = 4u;
+            if (const char *e = getenv("LZF_GPU_HOST_CAND_PARTS")) nparts = (uint32_t)strtoul(e, nullptr, 10);
+            if (nparts > 16u) nparts = 16u;
+            if (nparts > n) nparts = n;
+            if (nparts < 2u) nparts = 0u;
+        }
+        run_part.clear();
+        uint32_t part_of_k = 0;
         uint64_t x = 0, y = 0;
         uint32_t max_len = 0;
         /* a decode chunk whose inputs' whole span is no larger than its
@@ -779,7 +854,7 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
          * gather's read requests would slow that D2H side */
         bool span = false;
         uint64_t slo = ~0ull, shi = 0;
-        if (!a.compress) {
+        if (!a.compress && !d_all) {
             uint64_t outb = 0;
             for (uint32_t k = 0; k < n; k++) {
                 const uint32_t i = v.at(k0 + k);
@@ -797,10 +872,13 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         for (uint32_t k = 0; k < n; k++) {
             const uint32_t i = v.at(k0 + k);
             const uint64_t so = a.in_off[i], ext = in_extent(a, i);
-            if (span) {
+            if (d_all) {
+                m_din[k] = apad + (so - alo);            /* in the batch's span, copied ahead */
+            } else if (span) {
                 m_din[k] = iruns[0].dev + (so - slo);
             } else if (!iruns.empty() && so >= iruns.back().host + iruns.back().len &&
-                       so - (iruns.back().host + iruns.back().len) <= 256u) {
+                       so - (iruns.back().host + iruns.back().len) <= 256u &&
+                       !(nparts && (uint64_t)k * nparts / n != part_of_k)) {
                 Run &r = iruns.back();
                 m_din[k] = r.dev + (so - r.host);
                 if (so + ext - r.host > r.len) r.len = so + ext - r.host;
@@ -808,8 +886,10 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
                 x = ((x + 15u) & ~15ull) + (((uintptr_t)in_map + so) & 15u);
                 iruns.push_back(Run{so, x, ext});
                 m_din[k] = x;
+                if (nparts) part_of_k = (uint32_t)((uint64_t)k * nparts / n);
+                run_part.push_back(part_of_k);
             }
-            if (m_din[k] + ext > x) x = m_din[k] + ext;           /* span: x ends at the span's end */
+            if (!d_all && m_din[k] + ext > x) x = m_din[k] + ext;   /* span: x ends at the span's end */
             const uint64_t oo = a.out_off[i];
             if (!a.compress && !oruns.empty() && oo == oruns.back().host + oruns.back().len) {
                 Run &r = oruns.back();
@@ -828,7 +908,7 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
             const uint32_t l = a.compress ? a.in_len[i] : a.out_cap[i];
             if (l > max_len) max_len = l;
         }
-        uint8_t *d_in = (uint8_t *)sl.d_in.get(x + 16);
+        uint8_t *d_in = d_all ? d_all : (uint8_t *)sl.d_in.get(x + 16);
         uint8_t *d_out = (uint8_t *)sl.d_out.get(y + 16);
         uint8_t *d_meta = (uint8_t *)sl.d_meta.get((size_t)n * mrec);
         const size_t res_off = (uint8_t *)(m_cap + n) - h_meta;
@@ -841,6 +921,31 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         /* the chunks' inputs cross the bus one chunk after the other (side by
          * side they would share the link and all arrive at the end): chunk
          * k's kernels then start when its own inputs are in */
+        LzfParts parts{0u, nullptr, nullptr};
+        if (nparts && iruns.size() > few) nparts = 0;       /* a gathered chunk arrives whole */
+        if (nparts) {
+            if (!c.in_stream) check(hipStreamCreateWithFlags(&c.in_stream, hipStreamNonBlocking), "hipStreamCreate");
+            while (c.in_ev.size() < nparts) {
+                hipEvent_t ev;
+                check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+                c.in_ev.push_back(ev);
+            }
+            if (round) check(hipStreamWaitEvent(c.in_stream, c.slot[prev_si].in_done, 0), "hipStreamWaitEvent");
+            part_end.assign(nparts, 0u);
+            for (uint32_t j = 0; j < nparts; j++) {
+                part_end[j] = (uint32_t)((uint64_t)n * (j + 1u) / nparts);
+                for (size_t r = 0; r < iruns.size(); r++)
+                    if (run_part[r] == j && iruns[r].len)
+                        check(hipMemcpyAsync(d_in + iruns[r].dev, a.in + iruns[r].host, iruns[r].len,
+                                             hipMemcpyHostToDevice, c.in_stream),
+                              "hipMemcpyAsync");
+                check(hipEventRecord(c.in_ev[j], c.in_stream), "hipEventRecord");
+            }
+            parts = LzfParts{nparts, part_end.data(), c.in_ev.data()};
+            /* the descriptors go up on the slot's stream; the kernels wait for the parts */
+        } else if (d_all) {
+            check(hipStreamWaitEvent(sl.stream, c.in_ev[round], 0), "hipStreamWaitEvent");
+        } else {
         if (round) check(hipStreamWaitEvent(sl.stream, c.slot[prev_si].in_done, 0), "hipStreamWaitEvent");
         if (iruns.size() <= few) {
             for (const Run &r : iruns)
@@ -850,7 +955,8 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         } else {
             check(lzf_launch_move(in_map, d_src, d_in, d_din, d_in_len, min_len, n, sl.stream), "gather launch");
         }
-        check(hipEventRecord(sl.in_done, sl.stream), "hipEventRecord");
+        }
+        check(hipEventRecord(sl.in_done, nparts ? c.in_stream : sl.stream), "hipEventRecord");
         LzfBatch b{};
         b.in = d_in;
         b.in_off = d_din;
@@ -864,7 +970,7 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         b.max_len = max_len;
         const bool tail = k0 >= tail_from;
         check(tail   ? lzf_route_compress_window(b, sl.stream)
-              : bulk ? lzf_route_compress_bulk(b, sl.stream, sl.scratch)
+              : bulk ? lzf_route_compress_bulk(b, sl.stream, sl.scratch, nparts ? &parts : nullptr)
                      : launch(a, b, sl.stream),
               "kernel launch");
         /* outputs cross the bus in chunk order too: side by side, the chunks
@@ -895,6 +1001,7 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         sl.busy = true;
     }
     for (uint32_t k = 0; k < NSLOT_ALL; k++) drain(c.slot[k]);
+    if (c.in_stream) check(hipStreamSynchronize(c.in_stream), "hipStreamSynchronize");
 }
 
 /* the [lo, hi) byte ranges a sub-batch reads and writes in the caller's arenas */

@@ -72,9 +72,18 @@ struct LzfRecScratch {
     uint64_t bstride;
 };
 
+/* a batch whose inputs arrive in parts (the registered host path): part p is
+ * values [end[p-1], end[p]) (end[-1] = 0), in once ev[p] has fired on its
+ * stream; kernel 1 of a part may start then, the parse after all of them */
+struct LzfParts {
+    uint32_t n;
+    const uint32_t *end;
+    const hipEvent_t *ev;
+};
+
 /* launchers, defined next to their kernels; return hipSuccess or the error */
 hipError_t lzf_launch_compress_table(const LzfBatch &b, hipStream_t s, void *scratch, size_t scratch_bytes,
-                                     uint32_t *chunks);
+                                     uint32_t *chunks, const LzfParts *parts = nullptr);
 size_t lzf_table_scratch_per_value(uint32_t max_len);
 bool lzf_table_compress_supported(uint32_t max_len);
 hipError_t lzf_launch_compress_wtab(const LzfBatch &b, hipStream_t s, void *scratch, size_t scratch_bytes,
@@ -120,7 +129,8 @@ bool lzf_device_ok(int dev);
 void lzf_scratch_release_all(void);
 /* compress with the routed generations whatever the batch size, on a private
  * scratch (lzf_scratch_create): the host pipeline's side-by-side chunks */
-hipError_t lzf_route_compress_bulk(const LzfBatch &b, hipStream_t s, void *scratch);
+hipError_t lzf_route_compress_bulk(const LzfBatch &b, hipStream_t s, void *scratch,
+                                   const LzfParts *parts = nullptr);
 /* window64 (one wave per value), and whether the default routing is in
  * force (no LZF_GPU_KERNEL override, the LDS lane order held) */
 hipError_t lzf_route_compress_window(const LzfBatch &b, hipStream_t s);

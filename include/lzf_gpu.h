@@ -108,9 +108,13 @@ int lzf_gpu_synth_fill(int kind, uint64_t seed, uint64_t first, uint64_t stride,
  *
  * Moving bytes: when both arenas' spans lie in ranges given to
  * lzf_host_register, no CPU copies a value byte (the GPU and its DMA engines
- * move them; the bytes of an output slot past out_len[i] are then
- * unspecified, as after a failed call).  Otherwise the library stages values
- * through its own pinned buffers.  Results are identical either way.
+ * move them; the bytes of an output slot past out_len[i] are then either
+ * left as they were or zeroed -- never bytes of another value).  Otherwise
+ * the library stages values through its own pinned buffers.  Results are
+ * identical either way.
+ *
+ * LZF_GPU_SPLIT=block gives entry g a contiguous span of the values instead
+ * of every G-th one (lzf_host_split_block below).
  */
 int lzf_host_compress_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
                             uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,

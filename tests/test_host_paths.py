@@ -280,7 +280,8 @@ def test_registered_tail_mode_64k(oracle, registered, monkeypatch, share, chunks
         r = -(-t // per)
         q = max(nch, -(-(count - t) // per))
         edges += [t * k // r for k in range(r)] + [t + (count - t) * k // q for k in range(q)]
-    for i in sorted(set(list(range(0, count, 97)) + [e + d for e in edges for d in (-1, 0)] + [count - 1])):
+    for i in sorted({i for i in list(range(0, count, 97)) + [e + d for e in edges for d in (-1, 0)] + [count - 1]
+                     if 0 <= i < count}):
         exp = oracle.compress(bytes(arena[i * n:(i + 1) * n]), n - 4)
         assert bytes(out_r[i * n:i * n + olen_r[i]]) == exp, i
 
@@ -353,15 +354,20 @@ def test_register_refused_unless_every_plan_device_maps(monkeypatch):
     gibson_amd.host_unregister(a)
 
 
-def test_registered_decode_leaves_no_stale_bytes(oracle, registered):
+@pytest.mark.parametrize("dchunk_mb,gapped", [(None, False), ("1", False), (None, True)],
+                         ids=["abutting-dma", "abutting-dma-chunks-inputs-ahead", "gapped-scatter"])
+def test_registered_decode_leaves_no_stale_bytes(oracle, registered, monkeypatch, dchunk_mb, gapped):
     # abutting output slots go back to the caller as DMA runs of whole slots:
     # a second batch into the same layout whose streams decode short or fail
     # must not carry the first batch's decoded bytes past its own out_len
-    # (they are zeroed on the device first)
+    # (they are zeroed on the device first); with 1 MiB decode chunks the
+    # batch's inputs go H2D ahead of its chunks (LZF_GPU_HOST_SPAN_MB)
+    if dchunk_mb:
+        monkeypatch.setenv("LZF_GPU_HOST_DCHUNK_MB", dchunk_mb)
     import gibson_amd
     count, n = 512, 4096
     vals = [synth(k % 6, 0x5EED00B7, k, n) for k in range(count)]
-    streams = [oracle.compress(v, n + 64) for v in vals]
+    streams = [oracle.compress(v, n + n // 16 + 64) for v in vals]   # every value fits (incompressible ones grow)
     pos, offs = 0, []
     for st in streams:
         offs.append(pos)
@@ -377,14 +383,20 @@ def test_registered_decode_leaves_no_stale_bytes(oracle, registered):
     ilen = np.array([len(st) for st in streams], np.uint32)
     gibson_amd.host_decompress_batch(inp, ioff, ilen, out, doff, np.full(count, n, np.uint32), dl, er)
     assert (dl == n).all() and bytes(out[:n]) == vals[0]
-    # the same slots again: every third stream truncated (fails), every third
-    # other one decoded into a cap of half its length (E2BIG)
+    # the same slots again, every third stream truncated (it fails, or ends
+    # early at a token boundary). Abutting slots go back as one DMA run of
+    # whole slots: the bytes past each out_len must be zeros, not the first
+    # batch's decoded bytes still in the device arena. Gapped slots (every
+    # third cap halved, E2BIG for some) go back by the scatter kernel, which
+    # writes exactly out_len bytes: the caller's own bytes stay.
     cut = ilen.copy()
     cut[0::3] = np.maximum(cut[0::3] // 2, 1)
     caps = np.full(count, n, np.uint32)
-    caps[1::3] = n // 2
+    if gapped:
+        caps[1::3] = n // 2
     out[:] = 0xA5
     gibson_amd.host_decompress_batch(inp, ioff, cut, out, doff, caps, dl, er)
+    short = 0
     for k in range(count):
         e = oracle.decompress(bytes(inp[offs[k]:offs[k] + cut[k]]), int(caps[k]))
         s = out[k * n:(k + 1) * n]
@@ -392,4 +404,7 @@ def test_registered_decode_leaves_no_stale_bytes(oracle, registered):
             assert dl[k] == 0 and er[k] == e[1], k
         else:
             assert bytes(s[:dl[k]]) == e[0], k
-        assert not (s[dl[k]:caps[k]] != 0).any(), k         # no stale device bytes
+        tail = s[dl[k]:caps[k]]
+        short += tail.size > 0
+        assert (tail == (0xA5 if gapped else 0)).all(), k    # no stale device bytes
+    assert short > count // 4

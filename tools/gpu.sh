@@ -23,6 +23,8 @@
 #   xo:K:N:C:COUNTS     routed generation vs window64 by batch size (tools/crossover.py)
 #   host[:reg]          PCIe-inclusive host-path rates (tools/host_path_bench.py); :reg registered only
 #   hostenv:LABEL:ENV:ARGS  tools/host_path_bench.py ARGS under ENV
+#   hostsplit           registered text64k / json4k on LZF_GPU_DEVICES=0,0, round-robin vs block split
+#   numa                registered text64k with the arenas bound to NUMA node 0, then node 1
 #   trace:LABEL:ARGS    kernel + copy timeline of tools/host_path_bench.py ARGS (tools/trace_timeline.py)
 #   gpus2               the N-rank bench path rehearsed with two ranks on the one device (gloo)
 #   calib               FETCH_SIZE / WRITE_SIZE calibration (tools/fetch_calib.hip, built as tools/fetch_calib_bin)
@@ -115,6 +117,21 @@ for st in "$@"; do
         fi
         timeout -k 10 300 python tools/host_path_bench.py $1 $2 $3 5 --register > $O/host_$4_reg.json 2> $O/host_$4_reg.err || exit 1
         cut -c1-300 $O/host_$4_reg.json; done ;;
+    hostsplit)
+      # round 6: the library's two splits over two workers on the one device
+      # (LZF_GPU_DEVICES=0,0), registered arenas, text64k and json4k
+      for w in "2 65536 65536 text64k" "1 4096 524288 json4k"; do set -- $w
+        for sp in rr block; do
+          LZF_GPU_SPLIT=$sp timeout -k 10 300 python tools/host_path_bench.py $1 $2 $3 5 --register --devices 0,0 > $O/host_$4_reg_dev00_$sp.json 2> $O/host_$4_reg_dev00_$sp.err || exit 1
+          python3 -c "import json;d=json.load(open('$O/host_$4_reg_dev00_$sp.json'));print('$4 $sp', d['split'], d['compress_GBps'], d['decompress_GBps'], d['roundtrip_GBps'], d['roundtrip_ok'])"
+        done; done ;;
+    numa)
+      # round 6: registered arenas placed on each NUMA node (the GPU sits on
+      # node 0): what a worker pays for an arena across the socket link
+      for node in 0 1; do
+        timeout -k 10 300 python tools/host_path_bench.py 2 65536 65536 5 --register --arena-node $node > $O/host_text64k_reg_node$node.json 2> $O/host_text64k_reg_node$node.err || { tail -3 $O/host_text64k_reg_node$node.err; exit 1; }
+        python3 -c "import json;d=json.load(open('$O/host_text64k_reg_node$node.json'));print('node $node', d['arena_node'], d['compress_GBps'], d['decompress_GBps'], d['roundtrip_GBps'], d['roundtrip_ok'])"
+      done ;;
     hostenv:*)
       # hostenv:LABEL:ENV:ARGS -- tools/host_path_bench.py ARGS under ENV (VAR=x,VAR2=y)
       IFS=: read -r _ lab envs args <<< "$st"; args=${args//,/ }; envs=${envs//,/ }

@@ -4,7 +4,7 @@ starts in the client buffer and ends in the trie-resident value).  Times
 lzf_host_compress_batch / lzf_host_decompress_batch on host arrays: staging
 into pinned memory, hipMemcpyAsync H2D, kernels, D2H, copy-out -- for
 DESIGN.md, never bench.py's `value`.
-usage: host_path_bench.py [KIND N COUNT REPS] [--register] [--devices LIST]
+usage: host_path_bench.py [KIND N COUNT REPS] [--register] [--devices LIST] [--arena-node N]
   --register  lzf_host_register the three arenas first (the GPU moves the
               values; no CPU packing)
   --devices   LZF_GPU_DEVICES for this process (e.g. 0,0 or all): value i to
@@ -22,10 +22,30 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def aligned(nbytes):
+def aligned(nbytes, node=None):
+    """page-aligned zero bytes; with `node`, their pages bound to that NUMA
+    node (mbind MPOL_BIND before the first touch)"""
     raw = np.zeros(nbytes + 8192, np.uint8)
     k = (-raw.ctypes.data) % 4096
-    return raw[k:k + nbytes]
+    a = raw[k:k + nbytes]
+    if node is not None:
+        libc = ctypes.CDLL(None, use_errno=True)
+        mask = ctypes.c_ulong(1 << node)
+        # mbind(addr, len, MPOL_BIND = 2, nodemask, maxnode, MPOL_MF_MOVE = 2) -- syscall 237 on x86_64
+        rc = libc.syscall(237, ctypes.c_void_p(a.ctypes.data), ctypes.c_ulong(nbytes), 2, ctypes.byref(mask),
+                          ctypes.c_ulong(64), 2)
+        if rc != 0:
+            raise OSError(ctypes.get_errno(), f"mbind to node {node} refused")
+    return a
+
+
+def page_node(a):
+    """the NUMA node holding the page at a's first byte (get_mempolicy
+    MPOL_F_NODE | MPOL_F_ADDR, syscall 239), or -1"""
+    libc = ctypes.CDLL(None, use_errno=True)
+    mode = ctypes.c_int(-1)
+    rc = libc.syscall(239, ctypes.byref(mode), None, ctypes.c_ulong(0), ctypes.c_void_p(a.ctypes.data), 3)
+    return mode.value if rc == 0 else -1
 
 
 def main():
@@ -33,6 +53,9 @@ def main():
     ap.add_argument("pos", nargs="*", default=["1", "4096", "65536", "5"])
     ap.add_argument("--register", action="store_true")
     ap.add_argument("--devices", default=None)
+    ap.add_argument("--arena-node", type=int, default=None,
+                    help="bind the three host arenas' pages to this NUMA node (what a worker on the other "
+                         "socket's GPU pays for an arena the caller allocated on its own node)")
     args = ap.parse_args()
     if args.devices:
         os.environ["LZF_GPU_DEVICES"] = args.devices      # read once, at the library's first host call
@@ -42,15 +65,17 @@ def main():
     syn = ctypes.CDLL(os.path.join(ROOT, "gibson_amd", "libgibson_synth.so"))
     syn.synth_fill.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                ctypes.c_uint32, ctypes.c_void_p]
-    arena = aligned(count * n)
+    arena = aligned(count * n, args.arena_node)
     seed = {0: 0x5EED0004, 1: 0x5EED0002, 2: 0x5EED0003, 3: 0x5EED0005}.get(kind, 0x5EED0002)
     syn.synth_fill(kind, seed, 0, count, n, arena.ctypes.data)
     off = np.arange(count, dtype=np.uint64) * n
     ln = np.full(count, n, np.uint32)
     cap = np.full(count, n - 4, np.uint32)
-    out = aligned(count * n)
+    out = aligned(count * n, args.arena_node)
     olen = np.zeros(count, np.uint32)
-    dec = aligned(count * n)
+    dec = aligned(count * n, args.arena_node)
+    out[::4096] = 0
+    dec[::4096] = 0                                    # first touch: the pages land on the bound node
     dlen = np.zeros(count, np.uint32)
     err = np.zeros(count, np.int32)
     reg_s = None
@@ -91,6 +116,8 @@ def main():
         for a in (arena, out, dec):
             gibson_amd.host_unregister(a)
     print(json.dumps({"path": path, "devices": plan, "register_s": reg_s,
+                      "split": gibson_amd.host_split_policy(),
+                      "arena_node": {"asked": args.arena_node, "first_page": [page_node(x) for x in (arena, out, dec)]},
                       "spread_last_rep": {"compress": [[v, round(ms, 2)] for v, ms in spread_c],
                                           "decompress": [[v, round(ms, 2)] for v, ms in spread_d]},
                       "kind": kind, "seed": hex(seed), "n": n, "count": count, "in_bytes": count * n,
