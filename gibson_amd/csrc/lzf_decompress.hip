@@ -380,14 +380,6 @@ __device__ __forceinline__ void cd_flush(const uint8_t *lds, uint32_t outr_off, 
 #ifndef CD_MARKAHEAD_PIPE           /* the pipe's consumer */
 #define CD_MARKAHEAD_PIPE 0
 #endif
-/* CD_GAHEAD (round 6, the FAR instances of tokpar64 only): group g + 1's
- * owner lookup -- its start-mark ballot and the ds_bpermute of its owner
- * info -- issued right after group g's window byte read, and group g + 2's
- * marks after it, so a group's chain no longer waits on its own owner
- * lookup (the marks are already a group ahead, CD_MARKAHEAD) */
-#ifndef CD_GAHEAD
-#define CD_GAHEAD 0
-#endif
 /* FAR (round 5): the window is a ring smaller than the 8 KiB that
  * back-references reach (src/lzf_d.c:95); a source more than a window behind
  * the group is read back from the output in HBM, where the flush put it (the
@@ -423,27 +415,6 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
         cd_fence();
         m = mark[lane];
     }
-    constexpr bool GA = FAR && CD_GAHEAD && MA && !PER;
-    /* GA: the owner index of output byte o from the marks in m, and the
-     * owner's info by ds_bpermute (tbase advances past the group's starts) */
-    auto owner = [&](uint32_t ob) {
-        const bool mine = (MT)m == (MT)ob;
-        const uint64_t S = cd_ballot(mine);
-        const uint32_t le = __builtin_amdgcn_mbcnt_hi((uint32_t)(S >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)S, 0u)) +
-                            (mine ? 1u : 0u);
-        const uint32_t k = tbase + le - 1u;
-        tbase += (uint32_t)__builtin_popcountll(S);
-        return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)tinfo);
-    };
-    uint32_t tNext = 0u;
-    if (GA && total) {
-        tNext = owner(O + lane);
-        cd_fence();
-        mark[min(Otm - (O + CD_LANES), CD_LANES)] = (MT)Otm;
-        cd_fence();
-        m = mark[lane];
-    }
     for (uint32_t g = 0; g < total; g += CD_LANES) {
         const uint32_t gb = O + g;                     /* group's first output offset */
         const uint32_t o = gb + lane;
@@ -452,20 +423,15 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
             cd_fence();
             m = mark[lane];
         }
-        uint32_t tInf, k = 0u;
-        if (GA) {
-            tInf = tNext;
-        } else {
         const bool mine = (MT)m == (MT)o;   /* 16-bit marks: a stream's output stays below 65536 */
         const uint64_t S = cd_ballot(mine);
         const uint32_t le = __builtin_amdgcn_mbcnt_hi((uint32_t)(S >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)S, 0u)) +
                             (mine ? 1u : 0u);
-        k = tbase + le - 1u;
+        const uint32_t k = tbase + le - 1u;
         tbase += (uint32_t)__builtin_popcountll(S);
-        tInf = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)tinfo);
-        }
-        if (MA && !GA) {
+        const uint32_t tInf = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)tinfo);
+        if (MA) {
             /* the next group's marks, in the shadow of this group's LDS
              * chain (they depend on nothing it writes; a group past the
              * round marks slot 64 only: no token starts there) */
@@ -493,15 +459,6 @@ __device__ __forceinline__ void cd_output(uint8_t *lds, uint32_t outr_off, uint3
         const uint32_t a = outr_off + (lit ? li : so & omask);
         const uint32_t q = so - gb;
         uint32_t b = lds[a];
-        if (GA) {
-            /* the next group's owner and the marks of the one after it, in
-             * the shadow of this group's byte read */
-            tNext = owner(o + CD_LANES);
-            cd_fence();
-            mark[min(Otm - (gb + 2u * CD_LANES), CD_LANES)] = (MT)Otm;
-            cd_fence();
-            m = mark[lane];
-        }
         if (FAR) {
             /* a source more than a window behind the group's start: out of the ring */
 #if CD_FAR2

@@ -259,9 +259,8 @@ struct Ctx {
     bool numa_bound = false;
     hipStream_t stream = nullptr;
     Buf d_in, d_out, d_meta;
-    /* registered decode: the whole batch's input span, copied ahead of the
-     * chunks on its own stream (one event per chunk's part) */
-    Buf d_span;
+    /* registered compress, tail mode: the routed chunk's inputs in parts on
+     * their own stream (one event per part) */
     hipStream_t in_stream = nullptr;
     std::vector<hipEvent_t> in_ev;
     Buf h_in{nullptr, 0, true}, h_out{nullptr, 0, true}, h_meta{nullptr, 0, true};
@@ -299,7 +298,7 @@ struct Ctx {
             sl.busy = false;
         }
         if (in_stream) (void)hipStreamSynchronize(in_stream);
-        for (Buf *b : {&d_in, &d_out, &d_meta, &h_in, &h_out, &h_meta, &d_span}) b->release();
+        for (Buf *b : {&d_in, &d_out, &d_meta, &h_in, &h_out, &h_meta}) b->release();
         if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
     }
     /* after a failure: wait for what is in flight, so the buffers are free */
@@ -738,55 +737,6 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
     }
     const uint32_t min_len = a.compress ? 0u : 1u;
 
-    /* Decode, several chunks: the inputs of the whole batch go H2D ahead of
-     * the chunks, one DMA piece per chunk on the context's input stream, so
-     * the compressed bytes cross the bus at once instead of one chunk per
-     * slot turn; each chunk's kernels wait for their piece only.  The D2H
-     * side then carries the decoded bytes alone once the (smaller) inputs
-     * are in.  Taken when the inputs' whole span, gaps included, is no
-     * larger than the outputs (as the per-chunk span below) and fits
-     * LZF_GPU_HOST_SPAN_MB (default 8192). */
-    uint8_t *d_all = nullptr;
-    uint64_t alo = ~0ull, ahi = 0, apad = 0;
-    if (!a.compress && bound.size() > 2) {
-        uint64_t outb = 0;
-        for (uint32_t k = 0; k < v.count; k++) {
-            const uint32_t i = v.at(k);
-            const uint64_t so = a.in_off[i], ext = in_extent(a, i);
-            if (so < alo) alo = so;
-            if (so + ext > ahi) ahi = so + ext;
-            outb += a.out_cap[i];
-        }
-        uint64_t span_cap = 8192ull << 20;
-        if (const char *e = getenv("LZF_GPU_HOST_SPAN_MB")) span_cap = (uint64_t)strtoull(e, nullptr, 10) << 20;
-        if (ahi > alo && ahi - alo <= outb && ahi - alo <= span_cap) {
-            apad = ((uintptr_t)in_map + alo) & 15u;
-            d_all = (uint8_t *)c.d_span.get(ahi - alo + apad + 16);
-            if (!c.in_stream) check(hipStreamCreateWithFlags(&c.in_stream, hipStreamNonBlocking), "hipStreamCreate");
-            while (c.in_ev.size() < bound.size()) {
-                hipEvent_t ev;
-                check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
-                c.in_ev.push_back(ev);
-            }
-            /* the span in chunk order: piece r ends where chunk r's inputs end */
-            uint64_t done = alo;
-            for (uint32_t r = 0; r + 1 < bound.size(); r++) {
-                uint64_t hi = done;
-                for (uint32_t k = bound[r]; k < bound[r + 1]; k++) {
-                    const uint32_t i = v.at(k);
-                    const uint64_t e = a.in_off[i] + in_extent(a, i);
-                    if (e > hi) hi = e;
-                }
-                if (hi > done)
-                    check(hipMemcpyAsync(d_all + apad + (done - alo), a.in + done, hi - done, hipMemcpyHostToDevice,
-                                         c.in_stream),
-                          "hipMemcpyAsync");
-                check(hipEventRecord(c.in_ev[r], c.in_stream), "hipEventRecord");
-                done = hi;
-            }
-        }
-    }
-
     auto drain = [&](Slot &sl) {
         if (!sl.busy) return;
         check(hipEventSynchronize(sl.done), "hipEventSynchronize");
@@ -854,7 +804,7 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
          * gather's read requests would slow that D2H side */
         bool span = false;
         uint64_t slo = ~0ull, shi = 0;
-        if (!a.compress && !d_all) {
+        if (!a.compress) {
             uint64_t outb = 0;
             for (uint32_t k = 0; k < n; k++) {
                 const uint32_t i = v.at(k0 + k);
@@ -872,9 +822,7 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
         for (uint32_t k = 0; k < n; k++) {
             const uint32_t i = v.at(k0 + k);
             const uint64_t so = a.in_off[i], ext = in_extent(a, i);
-            if (d_all) {
-                m_din[k] = apad + (so - alo);            /* in the batch's span, copied ahead */
-            } else if (span) {
+            if (span) {
                 m_din[k] = iruns[0].dev + (so - slo);
             } else if (!iruns.empty() && so >= iruns.back().host + iruns.back().len &&
                        so - (iruns.back().host + iruns.back().len) <= 256u &&
@@ -889,7 +837,7 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
                 if (nparts) part_of_k = (uint32_t)((uint64_t)k * nparts / n);
                 run_part.push_back(part_of_k);
             }
-            if (!d_all && m_din[k] + ext > x) x = m_din[k] + ext;   /* span: x ends at the span's end */
+            if (m_din[k] + ext > x) x = m_din[k] + ext;           /* span: x ends at the span's end */
             const uint64_t oo = a.out_off[i];
             if (!a.compress && !oruns.empty() && oo == oruns.back().host + oruns.back().len) {
                 Run &r = oruns.back();
@@ -908,7 +856,7 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
             const uint32_t l = a.compress ? a.in_len[i] : a.out_cap[i];
             if (l > max_len) max_len = l;
         }
-        uint8_t *d_in = d_all ? d_all : (uint8_t *)sl.d_in.get(x + 16);
+        uint8_t *d_in = (uint8_t *)sl.d_in.get(x + 16);
         uint8_t *d_out = (uint8_t *)sl.d_out.get(y + 16);
         uint8_t *d_meta = (uint8_t *)sl.d_meta.get((size_t)n * mrec);
         const size_t res_off = (uint8_t *)(m_cap + n) - h_meta;
@@ -943,8 +891,6 @@ void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *
             }
             parts = LzfParts{nparts, part_end.data(), c.in_ev.data()};
             /* the descriptors go up on the slot's stream; the kernels wait for the parts */
-        } else if (d_all) {
-            check(hipStreamWaitEvent(sl.stream, c.in_ev[round], 0), "hipStreamWaitEvent");
         } else {
         if (round) check(hipStreamWaitEvent(sl.stream, c.slot[prev_si].in_done, 0), "hipStreamWaitEvent");
         if (iruns.size() <= few) {

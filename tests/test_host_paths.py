@@ -355,13 +355,12 @@ def test_register_refused_unless_every_plan_device_maps(monkeypatch):
 
 
 @pytest.mark.parametrize("dchunk_mb,gapped", [(None, False), ("1", False), (None, True)],
-                         ids=["abutting-dma", "abutting-dma-chunks-inputs-ahead", "gapped-scatter"])
+                         ids=["abutting-dma", "abutting-dma-chunks", "gapped-scatter"])
 def test_registered_decode_leaves_no_stale_bytes(oracle, registered, monkeypatch, dchunk_mb, gapped):
     # abutting output slots go back to the caller as DMA runs of whole slots:
     # a second batch into the same layout whose streams decode short or fail
     # must not carry the first batch's decoded bytes past its own out_len
-    # (they are zeroed on the device first); with 1 MiB decode chunks the
-    # batch's inputs go H2D ahead of its chunks (LZF_GPU_HOST_SPAN_MB)
+    # (they are zeroed on the device first); also with 1 MiB decode chunks
     if dchunk_mb:
         monkeypatch.setenv("LZF_GPU_HOST_DCHUNK_MB", dchunk_mb)
     import gibson_amd
