@@ -1122,6 +1122,10 @@ std::vector<Worker *> &workers()
     std::lock_guard<std::mutex> lk(mu);
     const std::vector<int> &dev = plan().dev;
     while (w.size() < dev.size()) {
+        /* LZF_GPU_FORCE_WORKER_FAIL=<entry>: making that entry's worker
+         * fails (tests of the partial-plan path) */
+        const char *ff = getenv("LZF_GPU_FORCE_WORKER_FAIL");
+        if (ff && *ff && (size_t)atoi(ff) == w.size()) throw std::bad_alloc();
         std::unique_ptr<Worker> x(new Worker(dev[w.size()]));
         w.push_back(x.get());
         x.release();

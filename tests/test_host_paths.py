@@ -407,3 +407,33 @@ def test_registered_decode_leaves_no_stale_bytes(oracle, registered, monkeypatch
         short += tail.size > 0
         assert (tail == (0xA5 if gapped else 0)).all(), k    # no stale device bytes
     assert short > count // 4
+
+
+def test_worker_plan_made_whole_or_not_at_all():
+    # LZF_GPU_DEVICES=0,0 with the second worker's creation failing
+    # (LZF_GPU_FORCE_WORKER_FAIL=1): the call returns LZF_GPU_ENOMEM and
+    # nothing runs on a partial plan; with the failure gone, the next call
+    # completes the plan and the batch is bit-exact against the oracle
+    code = ("import os, numpy as np, gibson_amd\n"
+            "from tests.oracle_lib import Oracle, synth\n"
+            "n, count = 4096, 64\n"
+            "a = np.frombuffer(b''.join(synth(k % 6, 0x5EED00B9, k, n) for k in range(count)), np.uint8).copy()\n"
+            "o = np.zeros(count * n, np.uint8); off = np.arange(count, dtype=np.uint64) * n\n"
+            "ln = np.full(count, n, np.uint32); cap = np.full(count, n - 4, np.uint32); ol = np.zeros(count, np.uint32)\n"
+            "L = gibson_amd.lib(); p = lambda x: x.ctypes.data\n"
+            "print(L.lzf_host_compress_batch(p(a), p(off), p(ln), p(o), p(off), p(cap), p(ol), count))\n"
+            "print(L.lzf_gpu_device_plan(None, None, None, 0))\n"
+            "del os.environ['LZF_GPU_FORCE_WORKER_FAIL']\n"
+            "print(L.lzf_host_compress_batch(p(a), p(off), p(ln), p(o), p(off), p(cap), p(ol), count))\n"
+            "print(L.lzf_gpu_device_plan(None, None, None, 0))\n"
+            "orc = Oracle()\n"
+            "bad = sum((bytes(o[k*n:k*n+ol[k]]) if ol[k] else None) != orc.compress(bytes(a[k*n:(k+1)*n]), n - 4)\n"
+            "          for k in range(count))\n"
+            "print(bad, [v for v, _ in gibson_amd.host_last_spread()])\n")
+    env = dict(os.environ, LZF_GPU_DEVICES="0,0", LZF_GPU_FORCE_WORKER_FAIL="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = r.stdout.split("\n")
+    assert out[0] == "-4" and out[1] == "-4", r.stdout           # ENOMEM: no partial plan runs
+    assert out[2] == "0" and out[3] == "2", r.stdout
+    assert out[4] == "0 [32, 32]", r.stdout
