@@ -547,7 +547,7 @@ __global__ __launch_bounds__(KT_THREADS) void lzf_cand_table_kernel(LzfBatch bt,
 #define K3_NRES    2u           /* candidate tests per loop iteration (2: 206.2 vs 210.8 ms for 1 + a memory-free one) */
 #endif
 #ifndef K3_RW
-#define K3_RW      32u          /* bitmap words kept in LDS per lane (power of two) */
+#define K3_RW      32u          /* bitmap words kept in LDS per lane (a multiple of 4) */
 #endif
 #ifndef K3_LITMIN
 #define K3_LITMIN   8u       /* lanes of the wave that must take a free-literal trip for it to run */
@@ -702,7 +702,7 @@ __global__ __launch_bounds__(K3_THREADS, K3_MINB) void lzf_parse_rec_kernel(LzfB
     uint32_t cw = 0u, curw = 0u;       /* inserted-bitmap word of p, in flight */
     __shared__ uint32_t k3_ring[K3_RW][K3_THREADS];
     uint32_t *const ring = &k3_ring[0][threadIdx.x];
-#define K3_RING(w_) ring[((w_) & (K3_RW - 1u)) * K3_THREADS]
+#define K3_RING(w_) ring[((w_) % K3_RW) * K3_THREADS]
     uint32_t fl = 0u;                  /* bitmap words [0, fl) are in scratch */
 #define K3_FLUSH_TO(w_)                                                            \
     do {                                                                           \
