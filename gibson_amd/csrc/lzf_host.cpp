@@ -322,12 +322,15 @@ struct Ctx {
     }
 };
 
-/* the calling thread's context, on the plan's first device */
+/* the calling thread's context, on the plan's first device, made on its
+ * first host-memory call (a thread that only uses the device-pointer calls
+ * never makes one: no stream or staging on a device it does not use) */
+thread_local std::unique_ptr<Ctx> t_caller;
 Ctx &caller_ctx()
 {
-    static thread_local Ctx c(plan().dev[0], false);
-    if (!c.ok) throw LzfFail{LZF_GPU_ENODEV};
-    return c;
+    if (!t_caller) t_caller.reset(new Ctx(plan().dev[0], false));
+    if (!t_caller->ok) throw LzfFail{LZF_GPU_ENODEV};
+    return *t_caller;
 }
 
 /* ---- registered host ranges (lzf_host_register) --------------------------- */
@@ -1115,10 +1118,12 @@ struct Worker {
  * that could not be had), the vector keeps the workers made so far, the
  * exception reaches the caller (who returns LZF_GPU_ENOMEM), and the next
  * call goes on from there -- no caller ever sees a partial plan. */
+std::mutex g_workers_mu;
+std::vector<Worker *> g_workers;
 std::vector<Worker *> &workers()
 {
-    static std::mutex mu;
-    static std::vector<Worker *> w;
+    std::mutex &mu = g_workers_mu;
+    std::vector<Worker *> &w = g_workers;
     std::lock_guard<std::mutex> lk(mu);
     const std::vector<int> &dev = plan().dev;
     while (w.size() < dev.size()) {
@@ -1450,18 +1455,14 @@ int lzf_host_last_spread(uint32_t *values, double *ms, int max)
 void lzf_gpu_release(void)
 {
     lzf_scratch_release_all();
-    try {
-        caller_ctx().release();
-    } catch (const LzfFail &) {
-    }
+    if (t_caller) t_caller->release();
     if (plan().rc == LZF_GPU_OK && plan().dev.size() > 1) {
-        std::vector<Worker *> *wp = nullptr;
-        try {
-            wp = &workers();
-        } catch (...) {
-            return;                                    /* no complete plan: nothing of it ran */
+        /* only the workers already made (release makes none) */
+        std::vector<Worker *> w;
+        {
+            std::lock_guard<std::mutex> lk(g_workers_mu);
+            w = g_workers;
         }
-        std::vector<Worker *> &w = *wp;
         Join j;
         j.left = (uint32_t)w.size();
         for (Worker *x : w)
