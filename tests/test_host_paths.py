@@ -239,9 +239,12 @@ def test_bad_device_plan_is_reported_not_aborted():
     assert r.stdout.split() == ["-3", "-3"], r.stdout
 
 
-@pytest.mark.parametrize("share,chunks,cap_mb", [(None, None, None), (50, 4, None), (None, None, 64), (None, None, 24)],
-                         ids=["default", "50pct-4chunks", "cap64MiB", "cap24MiB-slot-reuse"])
-def test_registered_tail_mode_64k(oracle, registered, monkeypatch, share, chunks, cap_mb):
+@pytest.mark.parametrize("share,chunks,cap_mb,scratch_mb",
+                         [(None, None, None, None), (50, 4, None, None), (None, None, 64, None), (None, None, 24, None),
+                          (None, None, None, 1140), (None, None, None, 1024)],
+                         ids=["default", "50pct-4chunks", "cap64MiB", "cap24MiB-slot-reuse",
+                              "scratch-table-2chunks", "scratch-lane"])
+def test_registered_tail_mode_64k(oracle, registered, monkeypatch, share, chunks, cap_mb, scratch_mb):
     # 256 MiB of 64 KiB values (configs[2]'s generator): the registered path's
     # tail mode -- the first part of the values through the table generation,
     # the rest by window64 in chunks beside its parse (default 70 % and one
@@ -255,6 +258,12 @@ def test_registered_tail_mode_64k(oracle, registered, monkeypatch, share, chunks
         monkeypatch.setenv("LZF_GPU_HOST_TAIL_CHUNKS", str(chunks))
     if cap_mb is not None:
         monkeypatch.setenv("LZF_GPU_HOST_CHUNK_MB", str(cap_mb))
+    if scratch_mb is not None:
+        # a scratch cap (each of the three slots holds a third): the routed
+        # chunk's cand parts then meet a table generation in two scratch
+        # chunks (1140 MiB) or the lane generation (1024 MiB), both of which
+        # wait for every input part before their first kernel
+        monkeypatch.setenv("LZF_GPU_SCRATCH_MB", str(scratch_mb))
     import gibson_amd
     from tests.oracle_lib import _SYN
     n, count = 65536, 4096
