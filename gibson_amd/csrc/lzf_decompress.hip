@@ -676,6 +676,12 @@ __global__ __launch_bounds__(64) void lzf_decompress_tokpar_kernel(LzfBatch bt, 
         } else {
             cd_stage<CD_IN_RING1>(inr, src, base, avail, loaded, lane);
         }
+#ifdef CD_DISC_TWICE                 /* diagnostics: the discovery's marginal cost (run twice, same result) */
+        {
+            const uint32_t x0 = cd_discover_lds<TSZT>(inr, imask, jt, base, in_len, lane);
+            asm volatile("" ::"v"(x0));
+        }
+#endif
         const uint32_t x = cd_discover_lds<TSZT>(inr, imask, jt, base, in_len, lane);
         const CdRound r = cd_decode(inr, imask, base, x, O, in_len, cap);
         if (r.err) {
