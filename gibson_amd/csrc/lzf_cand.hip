@@ -1092,7 +1092,7 @@ hipError_t lzf_launch_compress_table(const LzfBatch &b, hipStream_t s, void *scr
     const bool cand_only = stg && *stg == '1';
     /* kernel 1: the per-value pipeline (lzf_cand_table_kernel); in the
      * diagnostic build LZF_GPU_TCAND=stream takes the stream kernel's record
-     * form instead (lzf_stream.hip, bit-exact, slower: DESIGN.md §4.6) */
+     * form instead (lzf_stream.hip, bit-exact, slower: DESIGN.md §4.2) */
 #ifdef LZF_DIAG
     const char *tc = getenv("LZF_GPU_TCAND");
     const bool stream = tc && !strcmp(tc, "stream");

@@ -90,7 +90,7 @@ def test_compress_writes_nothing_past_out_cap(oracle, nmax):
 @pytest.mark.parametrize("nmax", [4096, 16384, 65536])
 def test_free_literal_runs_at_tight_caps(oracle, nmax):
     # whole waves of random and mixed-entropy values, so the parses'
-    # free-literal path (at least 8 lanes of a wave at a
+    # free-literal path (profiles/r03/INDEX.md: at least 8 lanes of a wave at a
     # literal with no candidate) runs, and caps that run out inside such runs
     rnd = random.Random(100 + nmax)
     vals, caps = [], []
