@@ -5,9 +5,8 @@
  * A 4 GiB buffer (beyond the 256 MiB Infinity Cache) allocated three ways --
  * hipMalloc (coarse-grained, L2-cached), hipExtMallocWithFlags Finegrained and
  * Uncached -- and, for each, 64 M accesses at random lines (every lane its own
- * line) of 4, 16 and 64 bytes (loads), 16-byte stores, and a dependent chain
- * (each lane's next line from the word it loaded: latency-bound, as the
- * parse's walk).  Prints G accesses per second.
+ * line) of 4, 16 and 64 bytes (loads) and 16-byte stores.  Prints G
+ * accesses per second.
  *   hipcc --offload-arch=gfx950 -O3 tools/probe/uc_probe.hip -o tools/probe/uc_probe_bin
  */
 #include <hip/hip_runtime.h>
@@ -46,14 +45,6 @@ __global__ __launch_bounds__(256) void scatter16(uint32_t *buf, uint32_t n)
     *p = make_uint4(i, i, i, i);
 }
 
-/* each lane walks `steps` dependent loads: the next line from the loaded word */
-__global__ __launch_bounds__(256) void chase(const uint32_t *buf, uint32_t steps, uint32_t *out)
-{
-    uint32_t x = line_of(blockIdx.x * blockDim.x + threadIdx.x);
-    for (uint32_t s = 0; s < steps; s++) x = line_of(buf[(uint64_t)x * 32u] + x + s);
-    if (x == 0x12345678u) out[0] = x;
-}
-
 __global__ void fill(uint32_t *buf, uint64_t words)
 {
     for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < words; k += (uint64_t)gridDim.x * blockDim.x)
@@ -82,26 +73,21 @@ int main()
         hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, 0, buf, (uint64_t)LINES * 32u);
         hipDeviceSynchronize();
         const dim3 g(n / 256u), b(256);
-        float ms[6];
-        for (int k = 0; k < 6; k++) {
+        float ms[4];
+        for (int k = 0; k < 4; k++) {
             for (int rep = 0; rep < 2; rep++) {
                 hipEventRecord(e0);
                 if (k == 0) hipLaunchKernelGGL(gather<4>, g, b, 0, 0, buf, n, out);
                 if (k == 1) hipLaunchKernelGGL(gather<16>, g, b, 0, 0, buf, n, out);
                 if (k == 2) hipLaunchKernelGGL(gather<64>, g, b, 0, 0, buf, n, out);
                 if (k == 3) hipLaunchKernelGGL(scatter16, g, b, 0, 0, buf, n);
-                if (k == 4) hipLaunchKernelGGL(chase, dim3(1024), b, 0, 0, buf, 256u, out);      /* 4 waves per SIMD */
-                if (k == 5) hipLaunchKernelGGL(chase, dim3(4096), b, 0, 0, buf, 256u, out);      /* 16 per SIMD */
                 hipEventRecord(e1);
                 hipEventSynchronize(e1);
                 hipEventElapsedTime(&ms[k], e0, e1);
             }
         }
-        printf("%-20s gather4 %6.1f  gather16 %6.1f  gather64 %6.1f  scatter16 %6.1f G/s | chase 4w/SIMD %6.1f G/s "
-               "(%.0f ns/step), 16w/SIMD %6.1f G/s (%.0f ns/step)\n",
-               names[t], n / ms[0] / 1e6, n / ms[1] / 1e6, n / ms[2] / 1e6, n / ms[3] / 1e6,
-               1024.0 * 256 * 256 / ms[4] / 1e6, ms[4] * 1e6 / 256, 4096.0 * 256 * 256 / ms[5] / 1e6,
-               ms[5] * 1e6 / 256);
+        printf("%-20s gather4 %6.1f  gather16 %6.1f  gather64 %6.1f  scatter16 %6.1f G/s\n", names[t],
+               n / ms[0] / 1e6, n / ms[1] / 1e6, n / ms[2] / 1e6, n / ms[3] / 1e6);
         hipFree(buf);
     }
     return 0;
