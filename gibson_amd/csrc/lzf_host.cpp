@@ -639,7 +639,7 @@ void host_batch_small(Ctx &c, const HostArgs &a, const View &v)
  * parse of a launch has a latency floor (~68 ms for 64 KiB values, DESIGN.md
  * §4.1) that mostly idles the GPU, so two or three overlapped launches cost
  * about one.  Compress batches of at least 192 MiB go in at least NSLOT
- * chunks (LZF_GPU_HOST_CHUNK_MB caps a chunk, default 2048) through the
+ * chunks (LZF_GPU_HOST_CHUNK_MB caps a chunk, default 4096) through the
  * routed generations whatever the chunk's count; decompress chunks hold
  * 256 MiB of output. */
 void host_batch_mapped(Ctx &c, const HostArgs &a, const View &v, const uint8_t *in_map, uint8_t *out_map)
