@@ -121,7 +121,10 @@ __device__ __forceinline__ uint32_t ln_ab(uint32_t hi, uint32_t lo)    /* (hi:lo
 
 __device__ __forceinline__ uint32_t ln_sel4(uint4 v, uint32_t i)
 {
-    return i == 0u ? v.x : i == 1u ? v.y : i == 2u ? v.z : v.w;
+    /* selects on the index bits: three v_cndmask, where an i == 0 / 1 / 2
+     * chain may become branches around a divergent index */
+    const uint32_t a = (i & 1u) ? v.y : v.x, b = (i & 1u) ? v.w : v.z;
+    return (i & 2u) ? b : a;
 }
 
 __device__ __forceinline__ uint32_t ln_first_diff(uint4 a, uint4 b)   /* 16 if equal */
@@ -892,7 +895,7 @@ __global__ __launch_bounds__(64) void lzf_cand_mid_kernel(LzfBatch bt, LzfLaneSc
 
 /* Diagnostic build only (-DK2_COUNT_SITES): per-site event counts of the
  * parse kernel's global memory accesses, summed over all lanes. */
-#if defined(K2_COUNT_SITES) || defined(KW_PHASES)
+#if defined(K2_COUNT_SITES) || defined(KW_PHASES) || defined(K2_WAVE_SITES)
 __device__ unsigned long long k2_sites[16];
 extern "C" int lzf_gpu_debug_sites(unsigned long long *out16, int reset)
 {
@@ -908,6 +911,17 @@ extern "C" int lzf_gpu_debug_sites(unsigned long long *out16, int reset)
 #define K2_SITE(i) atomicAdd(&k2_sites[i], 1ull)
 #else
 #define K2_SITE(i) ((void)0)
+#endif
+/* -DK2_WAVE_SITES: how often the WAVE runs each section of the lane parse
+ * (once per wave pass, whatever its active lanes), in k2_sites[0..15] */
+#ifdef K2_WAVE_SITES
+#define K2_WS(i)                                                                   \
+    do {                                                                           \
+        const uint64_t b_ = __ballot(1);                                           \
+        if ((b_ & (~b_ + 1ull)) == (1ull << (threadIdx.x & 63u))) wsc_[i]++;       \
+    } while (0)
+#else
+#define K2_WS(i) ((void)0)
 #endif
 /* -DKW_PHASES: cycles per phase of the wave-form parse, summed in k2_sites[0..7] */
 #ifdef KW_PHASES
@@ -966,22 +980,27 @@ __device__ __forceinline__ uint32_t k2_comb(uint32_t rel, uint32_t code)
 
 __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt, LzfLaneScratch sc)
 {
-    const uint32_t v = blockIdx.x * K2_THREADS + threadIdx.x;
-    if (v >= bt.count) return;
-    const uint32_t n = bt.in_len[v], cap = bt.out_cap[v];
-    /* src/lzf_c.c:131; past the stated max_len (the scratch stride): refused */
-    if (n == 0u || cap == 0u || n > bt.max_len) { bt.out_len[v] = 0u; return; }
-    const uint8_t *src = bt.in + bt.in_off[v];
-    uint8_t *dst = bt.out + bt.out_off[v];
-    const uint16_t *cand = sc.cand + (uint64_t)v * sc.cstride;
-    uint32_t *bits = sc.bits + (uint64_t)v * sc.bstride;
+    /* Persistent lanes: as many blocks as stay resident, lane l parsing
+     * values l, l + G, l + 2G, ... (G lanes in the grid), so a wave stays
+     * full while values remain: a wave's pass costs its instructions whatever
+     * its active lanes, and one value's chain can be ~2x another's (mixed
+     * data: 6.1 k wave passes for 3.4 k per value, profiles/r06/o).  A queue
+     * handing out values as lanes finish balanced mixed data ~3 % better and
+     * cost text and json 5-7 %: a load waits behind its lane's atomic
+     * (profiles/r06/p-r). */
+    uint32_t v = blockIdx.x * K2_THREADS + threadIdx.x;
+    uint32_t n = 0u, cap = 0u;
+    const uint8_t *src = nullptr;
+    uint8_t *dst = nullptr;
+    const uint16_t *cand = nullptr;
+    uint32_t *bits = nullptr;
 
     /* output: aligned dwords at da; acc holds the bytes from dword fw on */
-    const uint32_t dm = (uint32_t)((uintptr_t)dst & 3u);
-    uint8_t *const da = dst - dm;
+    uint32_t dm = 0u;
+    uint8_t *da = nullptr;
     uint64_t acc = 0;
-    uint32_t accn = dm, fw = 0;
-    uint32_t hx = dm;                   /* header byte of the open run (index from da) */
+    uint32_t accn = 0u, fw = 0;
+    uint32_t hx = 0u;                   /* header byte of the open run (index from da) */
     /* completed dwords [fs, fw) wait in pb0..2 and go out as one 16-byte
      * store: every store instruction of the wave touches 64 lines (one
      * per lane's value), so fewer, wider stores */
@@ -998,7 +1017,8 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
     uint4 C0 = W, C1 = W, C2 = W, C3 = W;
     uint32_t cw = 0u, curw = 0u;       /* inserted-bitmap word of p, in flight */
     /* the last K2_RW bitmap words of the value in LDS (word w at slot w % K2_RW,
-     * lane-interleaved: conflict-free), older words in the scratch array */
+     * lane-interleaved: conflict-free), older words in the scratch array;
+     * only words [fl, cw) of the current value are ever read from it */
     __shared__ uint32_t k2_ring[K2_RW][K2_THREADS];
     uint32_t *const ring = &k2_ring[0][threadIdx.x];
 #define K2_RING(w_) ring[((w_) & (K2_RW - 1u)) * K2_THREADS]
@@ -1015,9 +1035,74 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
     } while (0)
     uint32_t ms = 0u, me = 0u;         /* the last match: [ms, me) */
     uint32_t rel = 0u, q = 0u, k = 0u, lim = 0u, m = 0u;
-    bool ok = true;
-    uint32_t mode = n >= 3u ? K2_STEP : K2_DONE;
+    bool ok = true, live = false;
+    uint32_t mode = K2_DONE;
     [[maybe_unused]] uint32_t fm = 0u, fmb = 0xFFFFFFE0u;   /* K2_LITB: candidate mask of block fmb */
+    /* the lane's next value */
+#define K2_NEXT() (v + gridDim.x * K2_THREADS)
+    /* The value after this one: its lengths and offsets are loaded when the
+     * parse of v passes 31/32 of it, so a lane that finishes rarely waits */
+    uint32_t nv = v, nn = 0u, ncap = 0u, rsv = 2u, tr2 = 0u;
+    uint64_t nio = 0u, noo = 0u;
+#define K2_LOAD_AHEAD()                                                            \
+    do {                                                                           \
+        if (nv < bt.count) {                                                       \
+            nn = bt.in_len[nv];                                                    \
+            ncap = bt.out_cap[nv];                                                 \
+            nio = bt.in_off[nv];                                                   \
+            noo = bt.out_off[nv];                                                  \
+        }                                                                          \
+        rsv = 2u;                                                                  \
+    } while (0)
+    /* take the value ahead, or the first after it that the parse does not
+     * refuse (src/lzf_c.c:131; past the stated max_len, the scratch stride),
+     * with its state fresh; none left: the lane idles */
+#define K2_START()                                                                 \
+    do {                                                                           \
+        live = false;                                                              \
+        for (;;) {                                                                 \
+            if (rsv != 2u) K2_LOAD_AHEAD();                                        \
+            if (nv >= bt.count) break;                                             \
+            v = nv;                                                                \
+            n = nn;                                                                \
+            cap = ncap;                                                            \
+            src = bt.in + nio;                                                     \
+            dst = bt.out + noo;                                                    \
+            nv = K2_NEXT();                                                        \
+            rsv = 0u;                                                              \
+            if (n != 0u && cap != 0u && n <= bt.max_len) {                         \
+                live = true;                                                       \
+                break;                                                             \
+            }                                                                      \
+            bt.out_len[v] = 0u;                                                    \
+        }                                                                          \
+        if (live) {                                                                \
+            cand = sc.cand + (uint64_t)v * sc.cstride;                             \
+            bits = sc.bits + (uint64_t)v * sc.bstride;                             \
+            dm = (uint32_t)((uintptr_t)dst & 3u);                                  \
+            da = dst - dm;                                                         \
+            acc = 0;                                                               \
+            accn = dm;                                                             \
+            fw = 0u;                                                               \
+            hx = dm;                                                               \
+            pb0 = pb1 = pb2 = fs = 0u;                                             \
+            wb = 0xFFFFFFF0u;                                                      \
+            o = 1u;                                                                \
+            run = p = 0u;                                                          \
+            cb = 0xFFFFFFE0u;                                                      \
+            cw = curw = fl = 0u;                                                   \
+            ms = me = 0u;                                                          \
+            ok = true;                                                             \
+            fmb = 0xFFFFFFE0u;                                                     \
+            tr2 = n - (n >> 5);                                                    \
+            mode = n >= 3u ? K2_STEP : K2_DONE;                                    \
+        } else {                                                                   \
+            mode = K2_DONE;                                                        \
+        }                                                                          \
+    } while (0)
+#ifdef K2_WAVE_SITES
+    uint32_t wsc_[16] = {0u};
+#endif
 
 /* completed dwords [fs, fw) wait in pb0..2 (slot fw - fs) and leave with
  * the fourth as one 16-byte store; slot and patch selects instead of
@@ -1091,8 +1176,13 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
         if (++run == LZF_MAX_LIT) { K2_PATCH(hx, LZF_MAX_LIT - 1u); run = 0u; o++; } \
     } while (0)
 
-    while (__ballot(mode != K2_DONE)) {
+    K2_LOAD_AHEAD();                   /* nv = v: the lane's first value */
+    K2_START();
+    while (__ballot(live)) {
         if (mode != K2_DONE) K2_SITE(0);
+        K2_WS(0);
+        /* the next value's lengths and offsets */
+        if (live && rsv != 2u && p >= tr2) K2_LOAD_AHEAD();
         /* ---- the cand word of p ------------------------------------------ */
         if (mode == K2_STEP) {                                            /* src/lzf_c.c:145 */
             if (p >= n - 2u) {
@@ -1100,8 +1190,10 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
             } else {
                 uint32_t d = p - cb;
                 K2_SITE(10);
+                K2_WS(1);
                 if (d >= K2_CB) {
                     K2_SITE(1);
+                    K2_WS(2);
                     cb = p & ~(K2_CB - 1u);
                     d = p - cb;
                     const uint4 *cp = (const uint4 *)(cand + cb);
@@ -1127,6 +1219,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
 #pragma unroll
         for (uint32_t rt_ = 0; rt_ < K2_NRES; rt_++) {
             if (mode == K2_RESOLVE) {
+                K2_WS(3);
                 uint32_t word;
                 if (q >= ms) {
                     word = (q > ms && q + 3u <= me) ? 0u : 0xFFFFFFFFu;         /* last match's interior */
@@ -1161,8 +1254,10 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
         }
         /* ---- literal, or the start of a back-reference ------------------- */
         if (mode == K2_DECIDE) {
+            K2_WS(4);
             curw |= 1u << (p & 31u);                                     /* p is inserted */
             if (!(rel >= 2u && p + 4u < n)) {                            /* src/lzf_c.c:151-166 */
+                K2_WS(5);
                 if (o >= cap) {                                          /* src/lzf_c.c:263 */
                     ok = false;
                     mode = K2_DONE;
@@ -1192,14 +1287,20 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                      * when cand word cb + j has a candidate (code != 0), made
                      * once per block on the path's first use of it */
                     if ((uint32_t)__builtin_popcountll(__ballot(true)) >= K2_LITMIN) {
+                        K2_WS(6);
                         if (fmb != cb) {
+                            K2_WS(7);
                             fm = 0u;
 #pragma unroll
-                            for (uint32_t i_ = 0; i_ < 16u; i_++) {
-                                const uint32_t w_ = ln_sel4(i_ < 4u ? C0 : i_ < 8u ? C1 : i_ < 12u ? C2 : C3, i_ & 3u);
-                                /* codes of the two words at bits 0-2 and 16-18; + 7 carries into bit 3 / 19 when nonzero */
-                                const uint32_t t_ = ((w_ >> 13) & 0x70007u) + 0x70007u;
-                                fm |= (((t_ >> 3) & 1u) | ((t_ >> 18) & 2u)) << (2u * i_);
+                            for (uint32_t k_ = 0; k_ < 8u; k_++) {
+                                const uint4 Ck_ = k_ < 2u ? C0 : k_ < 4u ? C1 : k_ < 6u ? C2 : C3;
+                                const uint32_t lo_ = ln_sel4(Ck_, (2u * k_) & 3u), hi_ = ln_sel4(Ck_, (2u * k_ + 1u) & 3u);
+                                /* the high bytes of cand words 4k..4k+3 (their codes in bits 5-7) */
+                                const uint32_t x_ = __builtin_amdgcn_perm(hi_, lo_, 0x07050301u);
+                                /* bit 7 of each byte: its code is nonzero; the multiply gathers
+                                 * bits 7, 15, 23, 31 into bits 28-31 (no carries reach them) */
+                                const uint32_t t_ = (x_ | (x_ << 1) | (x_ << 2)) & 0x80808080u;
+                                fm |= ((t_ * 0x00204081u) >> 28) << (4u * k_);
                             }
                             fmb = cb;
                         }
@@ -1217,6 +1318,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                             }
                             go = r_ != 0u;
                             if ((uint32_t)__builtin_popcountll(__ballot(go)) < K2_LITMIN) break;
+                            K2_WS(8);
                             if (go) {
                                 K2_SITE(9);
                                 curw |= ((1u << r_) - 1u) << (p & 31u);
@@ -1276,6 +1378,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
 #endif
                 }
             } else {
+                K2_WS(9);
                 uint32_t maxlen = n - p - 2u;                            /* src/lzf_c.c:169-170 */
                 if (maxlen > LZF_MAX_REF) maxlen = LZF_MAX_REF;
                 lim = (maxlen > 16u && maxlen < 19u) ? 19u : maxlen;
@@ -1290,6 +1393,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
         }
         /* ---- one 16-byte piece of a long match --------------------------- */
         if (mode == K2_EXTEND) {
+            K2_WS(10);
             if (k < lim) {
                 K2_SITE(7);
                 const uint32_t avail = n - (p + k);
@@ -1307,6 +1411,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
         }
         /* ---- the back-reference ------------------------------------------ */
         if (mode == K2_EMIT) {
+            K2_WS(11);
             const uint32_t off = p - q - 1u;
             if (run) K2_PATCH(hx, run - 1u);                             /* close the run */
             else o--;                                                    /* undo empty run */
@@ -1334,6 +1439,7 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                     if (nw == cw) {
                         curw |= b1 | b2;
                     } else {
+                        K2_WS(12);
                         uint32_t wo = curw, wm = 0u, wn = 0u;
                         if ((t1 >> 5) == cw) wo |= b1; else if ((t1 >> 5) == nw) wn |= b1; else wm |= b1;
                         if ((t2 >> 5) == cw) wo |= b2; else if ((t2 >> 5) == nw) wn |= b2; else wm |= b2;
@@ -1351,24 +1457,35 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
                 }
             }
         }
+        /* ---- a finished value: its tail (src/lzf_c.c:276-290), then the next */
+        if (live && mode == K2_DONE) {
+            if (!ok || o + 3u > cap) {                                    /* src/lzf_c.c:276 */
+                bt.out_len[v] = 0u;
+            } else {
+                while (p < n) {                                           /* src/lzf_c.c:279-288 */
+                    K2_LITERAL(p);
+                    p++;
+                }
+                if (run) K2_PATCH(hx, run - 1u);
+                else o--;
+                for (uint32_t i = fs; i < fw; i++) {
+                    const uint32_t wv = i == fs ? pb0 : i == fs + 1u ? pb1 : pb2;
+                    if (i == 0u && dm != 0u)
+                        for (uint32_t t = dm; t < 4u; t++) da[t] = (uint8_t)(wv >> (8u * t));
+                    else
+                        *(uint32_t *)(da + 4u * i) = wv;
+                }
+                for (uint32_t t = 0; t < accn; t++)
+                    if (4u * fw + t >= dm) da[4u * fw + t] = (uint8_t)(acc >> (8u * t));
+                bt.out_len[v] = o;
+            }
+            K2_START();
+        }
     }
-    if (!ok || o + 3u > cap) { bt.out_len[v] = 0u; return; }          /* src/lzf_c.c:276 */
-    while (p < n) {                                                   /* src/lzf_c.c:279-288 */
-        K2_LITERAL(p);
-        p++;
-    }
-    if (run) K2_PATCH(hx, run - 1u);
-    else o--;
-    for (uint32_t i = fs; i < fw; i++) {
-        const uint32_t wv = i == fs ? pb0 : i == fs + 1u ? pb1 : pb2;
-        if (i == 0u && dm != 0u)
-            for (uint32_t t = dm; t < 4u; t++) da[t] = (uint8_t)(wv >> (8u * t));
-        else
-            *(uint32_t *)(da + 4u * i) = wv;
-    }
-    for (uint32_t t = 0; t < accn; t++)
-        if (4u * fw + t >= dm) da[4u * fw + t] = (uint8_t)(acc >> (8u * t));
-    bt.out_len[v] = o;
+#ifdef K2_WAVE_SITES
+    for (uint32_t i_ = 0; i_ < 16u; i_++)
+        if (wsc_[i_]) atomicAdd(&k2_sites[i_], (unsigned long long)wsc_[i_]);
+#endif
 #undef K2_STORE16
 #undef K2_PUT
 #undef K2_PATCH
@@ -1376,6 +1493,9 @@ __global__ __launch_bounds__(K2_THREADS) void lzf_parse_lane_kernel(LzfBatch bt,
 #undef K2_LITERAL
 #undef K2_RING
 #undef K2_FLUSH_TO
+#undef K2_NEXT
+#undef K2_LOAD_AHEAD
+#undef K2_START
 }
 
 #ifdef LZF_DIAG   /* wave-form parse: cross-check form */
@@ -1740,6 +1860,23 @@ bool lzf_lane_compress_supported(uint32_t max_len)
 #endif
 }
 
+/* blocks of the lane parse resident on the whole device at once (0: unknown);
+ * LZF_GPU_PARSE_RESIDENT overrides it (diagnostics) */
+static uint32_t parse_resident(size_t lds)
+{
+    if (const char *e = getenv("LZF_GPU_PARSE_RESIDENT")) return (uint32_t)strtoul(e, nullptr, 10);
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)lzf_parse_lane_kernel, (int)K2_THREADS,
+                                                     lds) != hipSuccess ||
+        cus <= 0 || per <= 0) {
+        (void)hipGetLastError();
+        return 0u;
+    }
+    return (uint32_t)cus * (uint32_t)per;
+}
+
 hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scratch,
                                     size_t scratch_bytes, uint32_t force_fix, hipStream_t aux,
                                     hipEvent_t *ev, uint32_t *chunks)
@@ -1857,8 +1994,13 @@ hipError_t lzf_launch_compress_lane(const LzfBatch &b, hipStream_t s, void *scra
             hipLaunchKernelGGL(lzf_parse_wave_kernel, dim3(cnt), dim3(64), 0, s2, c, sc[h]);
         else
 #endif
-            hipLaunchKernelGGL(lzf_parse_lane_kernel, dim3((cnt + K2_THREADS - 1u) / K2_THREADS),
-                               dim3(K2_THREADS), parse_lds, s2, c, sc[h]);
+        {
+            /* persistent lanes: as many blocks as stay resident */
+            uint32_t grid = (cnt + K2_THREADS - 1u) / K2_THREADS;
+            const uint32_t res = parse_resident(parse_lds);
+            if (res && grid > res) grid = res;
+            hipLaunchKernelGGL(lzf_parse_lane_kernel, dim3(grid), dim3(K2_THREADS), parse_lds, s2, c, sc[h]);
+        }
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (pipe && (e = hipEventRecord(ev[2 + h], aux)) != hipSuccess) return e;
     }
