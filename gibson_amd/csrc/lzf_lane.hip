@@ -942,11 +942,13 @@ extern "C" int lzf_gpu_debug_sites(unsigned long long *out16, int reset)
 #ifndef K2_NRES
 #define K2_NRES 1u
 #endif
+/* one trip taken when 6 lanes gain from it: with the persistent lanes, 2 trips
+ * / 8 lanes cost json4k, mixed16k and text8k 1.6-2.7 % (profiles/r06/v) */
 #ifndef K2_LITMIN
-#define K2_LITMIN   8u       /* lanes of the wave that must take a free-literal trip for it to run */
+#define K2_LITMIN   6u       /* lanes of the wave that must take a free-literal trip for it to run */
 #endif
 #ifndef K2_LITX
-#define K2_LITX 2u       /* free-literal trips after a literal in the same iteration (0: none) */
+#define K2_LITX 1u       /* free-literal trips after a literal in the same iteration (0: none) */
 #endif
 #ifndef K2_LITB
 #define K2_LITB 1        /* a trip takes up to 4 free literals (0: one) */
